@@ -1,0 +1,184 @@
+/*
+ * lgcn.h — C ABI of liblgcn.so, the MI355X (gfx950) LightGCN propagation library.
+ *
+ * This is the drop-in boundary for the reference's hot path: K-layer LightGCN message
+ * passing, i.e. torch_geometric.nn.LGConv (PyG 2.4.0) called once per layer from
+ * LightGCN.forward (reference models/light_gcn.py:24,32-34), plus the gradient that
+ * autograd takes through it during utils/train_test.py:train (reference
+ * utils/train_test.py:90-96).
+ *
+ * The reference has no FFI of its own (it is pure Python over PyG/ATen); the entry points
+ * below are exactly what a ctypes binding of this path needs (INTEGRATION.md shows it):
+ * plain pointers, sizes and a HIP stream, no torch types.
+ *
+ * Conventions
+ *   - Every function returns 0 on success, a positive hipError_t on a HIP failure, or a
+ *     negative LGCN_E_* code on an argument error; lgcn_last_error() describes the last
+ *     failure on the calling thread.
+ *   - The library never allocates or frees device memory and never synchronises: the
+ *     caller owns every buffer (including workspaces) and all work is ordered on the
+ *     caller's stream, so every call is hipGraph-capturable.
+ *   - Node ids are int64 on input (as edge_index is LongTensor[2,E] in the reference);
+ *     inside a plan they are int32 (N < 2^31) and CSR offsets are int64.
+ *   - Embedding tables are row-major fp32 [rows, d]. A "split" table is two pointers
+ *     (lo, hi) and a split row S: row r lives at lo + r*d when r < S, else at
+ *     hi + (r - S)*d. This lets layer 0 read user_embedding.weight and
+ *     item_embedding.weight in place instead of materialising torch.cat
+ *     (reference models/light_gcn.py:29).
+ */
+#ifndef LGCN_H
+#define LGCN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* lgcn_stream_t; /* a hipStream_t; NULL = the null stream */
+
+#define LGCN_ABI_VERSION 1
+
+#define LGCN_OK 0
+#define LGCN_E_ARG (-1)         /* bad size / null pointer / unsupported argument */
+#define LGCN_E_WORKSPACE (-2)   /* workspace smaller than lgcn_*_workspace_size() said */
+#define LGCN_E_UNSUPPORTED (-3) /* d or E outside what the kernels handle */
+
+/* One load-balanced unit of propagation work: edges [beg, beg+len) of one CSR row.
+ * dst >= 0: the whole row, write the epilogue for row dst.
+ * dst <  0: one chunk of a split row, write its partial sum to partial slot (-dst-1). */
+typedef struct {
+    int64_t beg;
+    int32_t len;
+    int32_t dst;
+} lgcn_item_t;
+
+/* A row whose edges were split into pcnt chunks; partials pbeg..pbeg+pcnt-1 (in edge order). */
+typedef struct {
+    int32_t row;
+    int32_t pbeg;
+    int32_t pcnt;
+    int32_t pad;
+} lgcn_split_t;
+
+/* Epilogue modes of lgcn_spmm. v = sum over the row's edges of val[e] * x[col[e]],
+ * accumulated sequentially in CSR order (the order CPU scatter_add_ uses).
+ *   INIT : y[r] = v (if y);  acc[r] = e[r] + v
+ *   ADD  : y[r] = v (if y);  acc[r] = acc[r] + v
+ *   FINAL_ACC : acc[r] = ((acc[r] + v) / div) * mul
+ *   FINAL_E   : acc[r] = ((e[r]  + v) / div) * mul
+ *   STORE     : acc[r] = v   (a bare LGConv layer)
+ * LightGCN forward with K layers (reference models/light_gcn.py:29-36):
+ *   layer 1 INIT(e=x0), layers 2..K-1 ADD, layer K FINAL_ACC(div=K+1, mul=fp32(1/(K+1)));
+ *   K == 1 uses FINAL_E(e=x0).
+ * Backward (autograd of the same): g = (dF*mul)/div, then K times INIT(e=g) over the
+ * transposed plan. */
+enum {
+    LGCN_EPI_INIT = 0,
+    LGCN_EPI_ADD = 1,
+    LGCN_EPI_FINAL_ACC = 2,
+    LGCN_EPI_FINAL_E = 3,
+    LGCN_EPI_STORE = 4
+};
+
+const char* lgcn_last_error(void);
+int lgcn_abi_version(void);
+
+/* ---------------------------------------------------------------------------------------
+ * CSR construction. Stable counting sort of the edge list by `key`:
+ *   rowptr[N+1] (int64), col[E] = other[perm] (int32), eid[E] = perm (int32),
+ * where perm lists edge positions grouped by key and, inside a key, in input order.
+ * Forward plan: key = edge_index[1] (target), other = edge_index[0] (source) — the
+ * per-target order in which PyG's scatter(reduce='sum') adds messages on CPU.
+ * Transposed plan (backward, reference Q3: train/val/test edge sets are asymmetric):
+ * key = edge_index[0], other = edge_index[1] — the order of index_add_ in
+ * index_select's backward.
+ * Out-of-range ids (<0 or >=N) set *err_count (device int64, caller-zeroed) > 0.
+ * Replaces: gcn_norm's degree scatter and scatter_add_'s implicit ordering inside
+ * LGConv.forward (PyG 2.4.0 nn/conv/lg_conv.py, nn/conv/gcn_conv.py::gcn_norm),
+ * called from reference models/light_gcn.py:33. */
+int lgcn_csr_workspace_size(int64_t E, int64_t N, size_t* bytes);
+int lgcn_csr_build(const int64_t* key, const int64_t* other, int64_t E, int64_t N,
+                   int64_t* rowptr, int32_t* col, int32_t* eid, int64_t* err_count,
+                   void* ws, size_t ws_bytes, lgcn_stream_t stream);
+
+/* gcn_norm(add_self_loops=False), PyG 2.4.0: deg = in-degree (count of edges whose target
+ * is the node), dis = deg^-1/2 with inf -> 0 (computed as 1/sqrt(deg), correctly rounded
+ * twice, which is what torch's CPU pow(-0.5) yields), and edge weight
+ * w = dis[source] * 1 * dis[target].
+ *   lgcn_inv_sqrt_degree: dis[i] from the FORWARD plan's rowptr (rows = targets).
+ *   lgcn_edge_norm: val[p] = dis[row(p)] * dis[col[p]] for every slot p of any plan
+ *   (forward or transposed; the product is symmetric). */
+int lgcn_inv_sqrt_degree(const int64_t* rowptr_fwd, int64_t N, float* dis, lgcn_stream_t stream);
+int lgcn_edge_norm(const int64_t* rowptr, const int32_t* col, int64_t N, int64_t E,
+                   const float* dis, float* val, lgcn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Load-balanced schedule for one plan. Rows longer than `chunk` edges are cut into chunks
+ * of `chunk` edges; items are ordered longest-first (stable), so neighbouring 16-lane groups
+ * of a wave carry equal work. Capacities: items <= N + E/chunk, splits <= N,
+ * partials <= E/chunk + N. counts[0..2] (device int64) receive n_items, n_splits,
+ * n_partials; the caller reads them back once per plan. */
+int lgcn_schedule_workspace_size(int64_t E, int64_t N, int32_t chunk, size_t* bytes);
+int lgcn_schedule_build(const int64_t* rowptr, int64_t N, int64_t E, int32_t chunk,
+                        lgcn_item_t* items, int64_t items_cap,
+                        lgcn_split_t* splits, int64_t splits_cap,
+                        int64_t* counts, void* ws, size_t ws_bytes, lgcn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * One propagation layer out = Â x with a fused LightGCN epilogue (see LGCN_EPI_*).
+ * Replaces LGConv.forward → propagate → message (w * x_j) → SumAggregation
+ * (PyG 2.4.0), reference models/light_gcn.py:33, and the layer-stack mean at :36 (folded
+ * into the epilogue), and — over the transposed plan — the autograd backward of both.
+ * x: split table (gather source). e: split table (epilogue addend; may be NULL unless the
+ * mode reads it). acc: split table (accumulator / final output). y: optional [N,d] layer
+ * output (input of the next layer). partial: [n_partials, d] scratch.
+ * Rows with no item still get nothing written: every row of the plan has at least one
+ * item (zero-length for zero in-degree), so the epilogue covers all N rows. */
+int lgcn_spmm(const lgcn_item_t* items, int64_t n_items,
+              const lgcn_split_t* splits, int64_t n_splits,
+              const int32_t* col, const float* val, int64_t N, int32_t d,
+              const float* x_lo, const float* x_hi, int64_t x_split,
+              const float* e_lo, const float* e_hi, int64_t e_split,
+              float* y,
+              float* acc_lo, float* acc_hi, int64_t acc_split,
+              float* partial, int32_t mode, float div, float mul,
+              lgcn_stream_t stream);
+
+/* The two halves of lgcn_spmm, same arguments: the item pass (every unsplit row's epilogue and
+ * every chunk partial) and the combine pass (split rows). lgcn_spmm == items then combine.
+ * Exposed so a profiler can bracket the dominant kernel alone. */
+int lgcn_spmm_items(const lgcn_item_t* items, int64_t n_items,
+                    const lgcn_split_t* splits, int64_t n_splits,
+                    const int32_t* col, const float* val, int64_t N, int32_t d,
+                    const float* x_lo, const float* x_hi, int64_t x_split,
+                    const float* e_lo, const float* e_hi, int64_t e_split,
+                    float* y,
+                    float* acc_lo, float* acc_hi, int64_t acc_split,
+                    float* partial, int32_t mode, float div, float mul,
+                    lgcn_stream_t stream);
+int lgcn_spmm_combine(const lgcn_item_t* items, int64_t n_items,
+                      const lgcn_split_t* splits, int64_t n_splits,
+                      const int32_t* col, const float* val, int64_t N, int32_t d,
+                      const float* x_lo, const float* x_hi, int64_t x_split,
+                      const float* e_lo, const float* e_hi, int64_t e_split,
+                      float* y,
+                      float* acc_lo, float* acc_hi, int64_t acc_split,
+                      float* partial, int32_t mode, float div, float mul,
+                      lgcn_stream_t stream);
+
+/* out[i] = (in[i] * mul) / div over n floats: the gradient that MulBackward (× 1/(K+1))
+ * then MeanBackward (÷ (K+1)) hand to every layer output (reference models/light_gcn.py:36). */
+int lgcn_scale(const float* in, float* out, int64_t n, float mul, float div, lgcn_stream_t stream);
+
+/* Split-table copy with scale: out[r] = (x[r] / div) * mul for r in [0,N) — the K == 0
+ * LightGCN forward (mean over a one-element stack). */
+int lgcn_copy_scale(const float* x_lo, const float* x_hi, int64_t x_split, int64_t N, int32_t d,
+                    float* out, float div, float mul, lgcn_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LGCN_H */

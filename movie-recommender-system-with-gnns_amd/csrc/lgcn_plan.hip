@@ -1,0 +1,336 @@
+// Plan construction for LightGCN propagation on gfx950: stable CSR build, gcn_norm edge
+// weights and the load-balanced work schedule. Runs once per edge set (the reference
+// recomputes gcn_norm on every layer call — reference models/light_gcn.py:33 via PyG 2.4.0
+// LGConv.forward — but the result is identical each time, so one plan per edge_index is
+// a legal cache).
+//
+// Everything is stream-ordered on the caller's stream, allocation-free and sync-free.
+
+#include <hipcub/hipcub.hpp>
+
+#include "lgcn_common.h"
+
+using namespace lgcn;
+
+namespace {
+
+// key32[e] = key[e], eid[e] = e; count ids outside [0, N).
+__global__ void k_prep_keys(const int64_t* __restrict__ key, const int64_t* __restrict__ other,
+                            int64_t E, int64_t N, int32_t* __restrict__ key32,
+                            int32_t* __restrict__ eid, unsigned long long* __restrict__ err) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    unsigned long long bad_local = 0;
+    for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < E; e += stride) {
+        const int64_t k = key[e];
+        const int64_t o = other[e];
+        const bool bad = (k < 0) | (k >= N) | (o < 0) | (o >= N);
+        bad_local += bad;
+        key32[e] = bad ? 0 : static_cast<int32_t>(k);
+        eid[e] = static_cast<int32_t>(e);
+    }
+    if (bad_local) atomicAdd(err, bad_local);
+}
+
+// rowptr from sorted keys: every row r in (keys[p-1], keys[p]] starts at slot p.
+__global__ void k_rowptr_from_sorted(const int32_t* __restrict__ keys, int64_t E, int64_t N,
+                                     int64_t* __restrict__ rowptr) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; p <= E; p += stride) {
+        const int64_t prev = (p == 0) ? -1 : keys[p - 1];
+        const int64_t cur = (p == E) ? N : keys[p];
+        for (int64_t r = prev + 1; r <= cur; ++r) rowptr[r] = p;
+    }
+}
+
+// col[p] = other[eid[p]]; an out-of-range id (already counted in err) becomes 0 so no later
+// pass of the build can read outside [0, N) before the caller sees the error.
+__global__ void k_gather_col(const int64_t* __restrict__ other, const int32_t* __restrict__ eid,
+                             int64_t E, int64_t N, int32_t* __restrict__ col) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; p < E; p += stride) {
+        const int64_t o = other[eid[p]];
+        col[p] = (o < 0 || o >= N) ? 0 : static_cast<int32_t>(o);
+    }
+}
+
+// PyG gcn_norm: deg = scatter(ones, target, reduce='sum') in fp32 — a sequential fp32 sum of
+// ones saturates at 2^24 — then deg.pow_(-0.5) (== 1/sqrt(deg), both correctly rounded, on
+// CPU) and inf -> 0.
+__global__ void k_inv_sqrt_degree(const int64_t* __restrict__ rowptr, int64_t N,
+                                  float* __restrict__ dis) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += stride) {
+        int64_t deg = rowptr[i + 1] - rowptr[i];
+        if (deg > (int64_t(1) << 24)) deg = int64_t(1) << 24;
+        const float degf = static_cast<float>(deg);
+        dis[i] = (deg == 0) ? 0.0f : 1.0f / sqrtf(degf);
+    }
+}
+
+__device__ __forceinline__ int64_t row_of_slot(const int64_t* __restrict__ rowptr, int64_t N,
+                                               int64_t p) {
+    // largest r in [0, N) with rowptr[r] <= p (then rowptr[r+1] > p)
+    int64_t lo = 0, hi = N - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (rowptr[mid] <= p) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// w = dis[source] * 1 * dis[target]; (dis[a]*1)*dis[b] == dis[a]*dis[b] exactly.
+__global__ void k_edge_norm(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                            int64_t N, int64_t E, const float* __restrict__ dis,
+                            float* __restrict__ val) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; p < E; p += stride) {
+        const int64_t r = row_of_slot(rowptr, N, p);
+        val[p] = dis[r] * dis[col[p]];
+    }
+}
+
+// ---- schedule ----
+__global__ void k_sched_count(const int64_t* __restrict__ rowptr, int64_t N, int32_t chunk,
+                              int64_t* __restrict__ n_items, int32_t* __restrict__ n_part,
+                              int32_t* __restrict__ n_split) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += stride) {
+        const int64_t deg = rowptr[i + 1] - rowptr[i];
+        const int64_t nch = (deg > chunk) ? (deg + chunk - 1) / chunk : 1;
+        n_items[i] = nch;
+        n_part[i] = (nch > 1) ? static_cast<int32_t>(nch) : 0;
+        n_split[i] = (nch > 1) ? 1 : 0;
+    }
+}
+
+__global__ void k_fill_u32(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+__global__ void k_sched_fill(const int64_t* __restrict__ rowptr, int64_t N, int32_t chunk,
+                             const int64_t* __restrict__ n_items, const int64_t* __restrict__ item_off,
+                             const int32_t* __restrict__ n_part, const int32_t* __restrict__ part_off,
+                             const int32_t* __restrict__ n_split, const int32_t* __restrict__ split_off,
+                             lgcn_item_t* __restrict__ raw, uint32_t* __restrict__ keys,
+                             int32_t* __restrict__ idx, lgcn_split_t* __restrict__ splits,
+                             int64_t* __restrict__ counts) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += stride) {
+        const int64_t beg = rowptr[i];
+        const int64_t deg = rowptr[i + 1] - beg;
+        const int64_t nch = n_items[i];
+        const int64_t off = item_off[i];
+        for (int64_t c = 0; c < nch; ++c) {
+            lgcn_item_t it;
+            it.beg = beg + c * chunk;
+            const int64_t rem = deg - c * chunk;
+            it.len = static_cast<int32_t>(rem < chunk ? rem : chunk);
+            it.dst = (nch > 1) ? -(part_off[i] + static_cast<int32_t>(c)) - 1 : static_cast<int32_t>(i);
+            raw[off + c] = it;
+            keys[off + c] = static_cast<uint32_t>(chunk - it.len);  // longest first
+            idx[off + c] = static_cast<int32_t>(off + c);
+        }
+        if (nch > 1) {
+            lgcn_split_t s;
+            s.row = static_cast<int32_t>(i);
+            s.pbeg = part_off[i];
+            s.pcnt = static_cast<int32_t>(nch);
+            s.pad = 0;
+            splits[split_off[i]] = s;
+        }
+        if (i == N - 1) {
+            counts[0] = off + nch;
+            counts[1] = split_off[i] + n_split[i];
+            counts[2] = part_off[i] + n_part[i];
+        }
+    }
+}
+
+__global__ void k_sched_gather(const lgcn_item_t* __restrict__ raw, const int32_t* __restrict__ idx,
+                               int64_t n, lgcn_item_t* __restrict__ items) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t m = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; m < n; m += stride)
+        items[m] = raw[idx[m]];
+}
+
+// sizes of the cub temp storage we need
+size_t csr_cub_bytes(int64_t E, int64_t N) {
+    size_t t = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                       (const int32_t*)nullptr, (int32_t*)nullptr,
+                                       static_cast<int>(E), 0, key_bits(N));
+    return t;
+}
+
+int64_t sched_items_cap(int64_t E, int64_t N, int32_t chunk) { return N + E / chunk + 1; }
+
+size_t sched_cub_bytes(int64_t E, int64_t N, int32_t chunk) {
+    const int64_t cap = sched_items_cap(E, N, chunk);
+    size_t a = 0, b = 0, c = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, (const int64_t*)nullptr, (int64_t*)nullptr,
+                                     static_cast<int>(N));
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                     static_cast<int>(N));
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                       (const int32_t*)nullptr, (int32_t*)nullptr,
+                                       static_cast<int>(cap), 0, key_bits(int64_t(chunk) + 2));
+    size_t m = a > b ? a : b;
+    return m > c ? m : c;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* lgcn_last_error(void) { return err_buf(); }
+int lgcn_abi_version(void) { return LGCN_ABI_VERSION; }
+
+int lgcn_csr_workspace_size(int64_t E, int64_t N, size_t* bytes) {
+    if (!bytes || E < 0 || N < 0) return fail(LGCN_E_ARG, "lgcn_csr_workspace_size: bad args");
+    if (E > INT32_MAX || N > INT32_MAX)
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_csr_workspace_size: E=%lld N=%lld exceed int32",
+                    (long long)E, (long long)N);
+    Carver c{nullptr, 0};
+    c.take<int32_t>(E);  // key32 in
+    c.take<int32_t>(E);  // key32 out
+    c.take<int32_t>(E);  // eid in
+    c.take<char>(csr_cub_bytes(E, N > 0 ? N : 1));
+    *bytes = c.used + 256;
+    return LGCN_OK;
+}
+
+int lgcn_csr_build(const int64_t* key, const int64_t* other, int64_t E, int64_t N,
+                   int64_t* rowptr, int32_t* col, int32_t* eid, int64_t* err_count, void* ws,
+                   size_t ws_bytes, lgcn_stream_t stream) {
+    if (E < 0 || N < 0 || !rowptr || !err_count || (E > 0 && (!key || !other || !col || !eid)))
+        return fail(LGCN_E_ARG, "lgcn_csr_build: bad args");
+    if (E > INT32_MAX || N > INT32_MAX)
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_csr_build: E=%lld N=%lld exceed int32",
+                    (long long)E, (long long)N);
+    hipStream_t s = as_stream(stream);
+    if (E == 0) {
+        int rc = check_hip(hipMemsetAsync(rowptr, 0, sizeof(int64_t) * (N + 1), s), "memset rowptr");
+        return rc;
+    }
+    Carver c{static_cast<char*>(ws), ws_bytes};
+    int32_t* k_in = c.take<int32_t>(E);
+    int32_t* k_out = c.take<int32_t>(E);
+    int32_t* e_in = c.take<int32_t>(E);
+    size_t cub_bytes = csr_cub_bytes(E, N);
+    void* cub_tmp = c.take<char>(cub_bytes);
+    if (!c.ok) return fail(LGCN_E_WORKSPACE, "lgcn_csr_build: workspace %zu < %zu", ws_bytes, c.used);
+
+    k_prep_keys<<<grid_for(E, kBlock, 8192), kBlock, 0, s>>>(
+        key, other, E, N, k_in, e_in, reinterpret_cast<unsigned long long*>(err_count));
+    if (int rc = check_launch("k_prep_keys")) return rc;
+    // LSD radix sort is stable: equal keys keep input (edge) order.
+    if (int rc = check_hip(hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k_in, k_out, e_in,
+                                                              eid, static_cast<int>(E), 0,
+                                                              key_bits(N), s),
+                           "SortPairs(csr)"))
+        return rc;
+    k_rowptr_from_sorted<<<grid_for(E + 1, kBlock, 8192), kBlock, 0, s>>>(k_out, E, N, rowptr);
+    if (int rc = check_launch("k_rowptr_from_sorted")) return rc;
+    k_gather_col<<<grid_for(E, kBlock, 8192), kBlock, 0, s>>>(other, eid, E, N, col);
+    return check_launch("k_gather_col");
+}
+
+int lgcn_inv_sqrt_degree(const int64_t* rowptr_fwd, int64_t N, float* dis, lgcn_stream_t stream) {
+    if (N < 0 || !rowptr_fwd || (N > 0 && !dis)) return fail(LGCN_E_ARG, "lgcn_inv_sqrt_degree: bad args");
+    if (N == 0) return LGCN_OK;
+    k_inv_sqrt_degree<<<grid_for(N, kBlock, 8192), kBlock, 0, as_stream(stream)>>>(rowptr_fwd, N, dis);
+    return check_launch("k_inv_sqrt_degree");
+}
+
+int lgcn_edge_norm(const int64_t* rowptr, const int32_t* col, int64_t N, int64_t E,
+                   const float* dis, float* val, lgcn_stream_t stream) {
+    if (N < 0 || E < 0 || !rowptr || (E > 0 && (!col || !dis || !val)))
+        return fail(LGCN_E_ARG, "lgcn_edge_norm: bad args");
+    if (E == 0) return LGCN_OK;
+    if (N == 0) return fail(LGCN_E_ARG, "lgcn_edge_norm: E > 0 with N == 0");
+    k_edge_norm<<<grid_for(E, kBlock, 8192), kBlock, 0, as_stream(stream)>>>(rowptr, col, N, E, dis, val);
+    return check_launch("k_edge_norm");
+}
+
+int lgcn_schedule_workspace_size(int64_t E, int64_t N, int32_t chunk, size_t* bytes) {
+    if (!bytes || E < 0 || N < 0 || chunk < 1) return fail(LGCN_E_ARG, "lgcn_schedule_workspace_size: bad args");
+    if (N > INT32_MAX || E > INT32_MAX) return fail(LGCN_E_UNSUPPORTED, "schedule: sizes exceed int32");
+    const int64_t cap = sched_items_cap(E, N, chunk);
+    Carver c{nullptr, 0};
+    c.take<int64_t>(N);          // n_items
+    c.take<int64_t>(N);          // item_off
+    c.take<int32_t>(N);          // n_part
+    c.take<int32_t>(N);          // part_off
+    c.take<int32_t>(N);          // n_split
+    c.take<int32_t>(N);          // split_off
+    c.take<lgcn_item_t>(cap);    // raw items
+    c.take<uint32_t>(cap);       // keys in
+    c.take<uint32_t>(cap);       // keys out
+    c.take<int32_t>(cap);        // idx in
+    c.take<int32_t>(cap);        // idx out
+    c.take<char>(sched_cub_bytes(E, N > 0 ? N : 1, chunk));
+    *bytes = c.used + 256;
+    return LGCN_OK;
+}
+
+int lgcn_schedule_build(const int64_t* rowptr, int64_t N, int64_t E, int32_t chunk,
+                        lgcn_item_t* items, int64_t items_cap, lgcn_split_t* splits,
+                        int64_t splits_cap, int64_t* counts, void* ws, size_t ws_bytes,
+                        lgcn_stream_t stream) {
+    if (!rowptr || !counts || N < 0 || E < 0 || chunk < 1)
+        return fail(LGCN_E_ARG, "lgcn_schedule_build: bad args");
+    if (N > INT32_MAX || E > INT32_MAX) return fail(LGCN_E_UNSUPPORTED, "schedule: sizes exceed int32");
+    hipStream_t s = as_stream(stream);
+    if (N == 0) return check_hip(hipMemsetAsync(counts, 0, 3 * sizeof(int64_t), s), "memset counts");
+    const int64_t cap = sched_items_cap(E, N, chunk);
+    if (!items || items_cap < cap || !splits || splits_cap < N)
+        return fail(LGCN_E_ARG, "lgcn_schedule_build: items_cap %lld < %lld or splits_cap %lld < %lld",
+                    (long long)items_cap, (long long)cap, (long long)splits_cap, (long long)N);
+    Carver c{static_cast<char*>(ws), ws_bytes};
+    int64_t* n_items = c.take<int64_t>(N);
+    int64_t* item_off = c.take<int64_t>(N);
+    int32_t* n_part = c.take<int32_t>(N);
+    int32_t* part_off = c.take<int32_t>(N);
+    int32_t* n_split = c.take<int32_t>(N);
+    int32_t* split_off = c.take<int32_t>(N);
+    lgcn_item_t* raw = c.take<lgcn_item_t>(cap);
+    uint32_t* k_in = c.take<uint32_t>(cap);
+    uint32_t* k_out = c.take<uint32_t>(cap);
+    int32_t* i_in = c.take<int32_t>(cap);
+    int32_t* i_out = c.take<int32_t>(cap);
+    size_t cub_bytes = sched_cub_bytes(E, N, chunk);
+    void* cub_tmp = c.take<char>(cub_bytes);
+    if (!c.ok) return fail(LGCN_E_WORKSPACE, "lgcn_schedule_build: workspace %zu < %zu", ws_bytes, c.used);
+
+    const unsigned g = grid_for(N, kBlock, 8192);
+    k_sched_count<<<g, kBlock, 0, s>>>(rowptr, N, chunk, n_items, n_part, n_split);
+    if (int rc = check_launch("k_sched_count")) return rc;
+    size_t t = cub_bytes;
+    if (int rc = check_hip(hipcub::DeviceScan::ExclusiveSum(cub_tmp, t, n_items, item_off, static_cast<int>(N), s), "scan items")) return rc;
+    t = cub_bytes;
+    if (int rc = check_hip(hipcub::DeviceScan::ExclusiveSum(cub_tmp, t, n_part, part_off, static_cast<int>(N), s), "scan parts")) return rc;
+    t = cub_bytes;
+    if (int rc = check_hip(hipcub::DeviceScan::ExclusiveSum(cub_tmp, t, n_split, split_off, static_cast<int>(N), s), "scan splits")) return rc;
+    // padding slots [n_items, cap) sort last (key = chunk + 1) and are never read
+    const uint32_t pad_key = static_cast<uint32_t>(chunk) + 1u;
+    k_fill_u32<<<grid_for(cap, kBlock, 8192), kBlock, 0, s>>>(k_in, cap, pad_key);
+    if (int rc = check_launch("k_fill_u32")) return rc;
+    k_fill_u32<<<grid_for(cap, kBlock, 8192), kBlock, 0, s>>>(reinterpret_cast<uint32_t*>(i_in), cap, 0u);
+    if (int rc = check_launch("k_fill_u32")) return rc;
+    k_sched_fill<<<g, kBlock, 0, s>>>(rowptr, N, chunk, n_items, item_off, n_part, part_off, n_split,
+                                      split_off, raw, k_in, i_in, splits, counts);
+    if (int rc = check_launch("k_sched_fill")) return rc;
+    t = cub_bytes;
+    if (int rc = check_hip(hipcub::DeviceRadixSort::SortPairs(cub_tmp, t, k_in, k_out, i_in, i_out,
+                                                              static_cast<int>(cap), 0,
+                                                              key_bits(int64_t(chunk) + 2), s),
+                           "SortPairs(schedule)"))
+        return rc;
+    // gather all cap slots; the tail beyond n_items is padding the kernels never index
+    k_sched_gather<<<grid_for(cap, kBlock, 8192), kBlock, 0, s>>>(raw, i_out, cap, items);
+    return check_launch("k_sched_gather");
+}
+
+}  // extern "C"

@@ -1,0 +1,382 @@
+// LightGCN propagation kernels for gfx950 (MI355X).
+//
+// One launch = one LGConv layer y = Â x over a plan's CSR (rows = destinations), fused with
+// the LightGCN layer-stack epilogue (reference models/light_gcn.py:29-36; Â is PyG 2.4.0's
+// gcn_norm-weighted adjacency, applied by LGConv.forward at :33).
+//
+// Mapping (d = 64 fp32, the headline config): a 256-thread workgroup = 4 waves = 16 groups of
+// 16 lanes; one group owns one schedule item (a whole row, or a <= chunk-edge piece of a long
+// row); each lane owns one float4 column slice, so one wave-instruction gathers 4 neighbour
+// rows (1 KiB) with global_load_dwordx4. Items are ordered longest-first, so the 4 groups of a
+// wave carry (nearly) equal work. Neighbour ids/weights are loaded once per 16-edge batch,
+// coalesced, and broadcast inside the group by cross-lane permute; UNROLL gathers are issued
+// before the first add, so every wave keeps several KiB in flight.
+//
+// Numerics: per row, v = (((0 + w0*x0) + w1*x1) + ...) in CSR order, mul then add (no FMA:
+// this file is built with -ffp-contract=off), i.e. the order and rounding of PyG's CPU
+// scatter_add_. Unsplit rows are therefore bit-identical to the reference CPU path; split rows
+// add chunk partials in chunk order (deterministic, within 1e-6 relative).
+// No atomics anywhere: every output row is written by exactly one group.
+
+#include "lgcn_common.h"
+
+using namespace lgcn;
+
+namespace {
+
+struct SpmmArgs {
+    const lgcn_item_t* items;
+    int64_t n_items;
+    const lgcn_split_t* splits;
+    int64_t n_splits;
+    const int32_t* col;
+    const float* val;
+    const float* x_lo;
+    const float* x_hi;
+    int64_t x_split;
+    const float* e_lo;
+    const float* e_hi;
+    int64_t e_split;
+    float* y;
+    float* acc_lo;
+    float* acc_hi;
+    int64_t acc_split;
+    float* partial;
+    int32_t d;
+    int32_t mode;
+    float div;
+    float mul;
+};
+
+template <class T>
+__device__ __forceinline__ T* split_row(T* lo, T* hi, int64_t split, int64_t r, int64_t stride) {
+    return (r < split) ? lo + r * stride : hi + (r - split) * stride;
+}
+
+__device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 f4_axpy(float4 acc, float w, float4 x) {
+    // acc + (w * x): two roundings, never contracted (-ffp-contract=off)
+    return make_float4(acc.x + w * x.x, acc.y + w * x.y, acc.z + w * x.z, acc.w + w * x.w);
+}
+__device__ __forceinline__ float4 f4_divmul(float4 a, float div, float mul) {
+    return make_float4((a.x / div) * mul, (a.y / div) * mul, (a.z / div) * mul, (a.w / div) * mul);
+}
+
+// Epilogue for one finished row r; lane l owns float4 slots l, l+LPR, ... (NV of them).
+template <int LPR, int NV>
+__device__ __forceinline__ void finish_row_vec(const SpmmArgs& a, int64_t r, int l, const float4 (&v)[NV]) {
+    const int64_t d4 = int64_t(LPR) * NV;
+    float4* acc = reinterpret_cast<float4*>(split_row(a.acc_lo, a.acc_hi, a.acc_split, r, a.d));
+    if (a.mode == LGCN_EPI_INIT || a.mode == LGCN_EPI_FINAL_E) {
+        const float4* e = reinterpret_cast<const float4*>(split_row(a.e_lo, a.e_hi, a.e_split, r, a.d));
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const float4 s = f4_add(e[l + k * LPR], v[k]);
+            acc[l + k * LPR] = (a.mode == LGCN_EPI_INIT) ? s : f4_divmul(s, a.div, a.mul);
+        }
+    } else if (a.mode == LGCN_EPI_STORE) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[l + k * LPR] = v[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const float4 s = f4_add(acc[l + k * LPR], v[k]);
+            acc[l + k * LPR] = (a.mode == LGCN_EPI_ADD) ? s : f4_divmul(s, a.div, a.mul);
+        }
+    }
+    if (a.y != nullptr && (a.mode == LGCN_EPI_INIT || a.mode == LGCN_EPI_ADD)) {
+        float4* y = reinterpret_cast<float4*>(a.y) + r * d4;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) y[l + k * LPR] = v[k];
+    }
+}
+
+template <int LPR, int NV, int UNROLL>
+__global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
+    constexpr int GPB = kBlock / LPR;  // groups per block
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    const int64_t item = int64_t(blockIdx.x) * GPB + g;
+    if (item >= a.n_items) return;  // whole group leaves together
+    const lgcn_item_t it = a.items[item];
+    const int64_t d4 = int64_t(LPR) * NV;
+    const float4* __restrict__ xlo = reinterpret_cast<const float4*>(a.x_lo);
+    const float4* __restrict__ xhi = reinterpret_cast<const float4*>(a.x_hi);
+
+    float4 acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    for (int b = 0; b < it.len; b += LPR) {
+        const int n = min(LPR, it.len - b);
+        int c = 0;
+        float w = 0.f;
+        if (l < n) {
+            c = a.col[it.beg + b + l];
+            w = a.val[it.beg + b + l];
+        }
+        int j = 0;
+        for (; j + UNROLL <= n; j += UNROLL) {
+            float4 xv[UNROLL][NV];
+            float wv[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const int cj = __shfl(c, j + u, LPR);
+                wv[u] = __shfl(w, j + u, LPR);
+                const float4* src = (cj < a.x_split) ? xlo + int64_t(cj) * d4
+                                                     : xhi + (int64_t(cj) - a.x_split) * d4;
+#pragma unroll
+                for (int k = 0; k < NV; ++k) xv[u][k] = src[l + k * LPR];
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+                for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wv[u], xv[u][k]);
+        }
+        for (; j < n; ++j) {
+            const int cj = __shfl(c, j, LPR);
+            const float wj = __shfl(w, j, LPR);
+            const float4* src = (cj < a.x_split) ? xlo + int64_t(cj) * d4
+                                                 : xhi + (int64_t(cj) - a.x_split) * d4;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wj, src[l + k * LPR]);
+        }
+    }
+
+    if (it.dst < 0) {
+        float4* p = reinterpret_cast<float4*>(a.partial) + int64_t(-it.dst - 1) * d4;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) p[l + k * LPR] = acc[k];
+        return;
+    }
+    finish_row_vec<LPR, NV>(a, it.dst, l, acc);
+}
+
+// Split rows: add the chunk partials in chunk (= edge) order, then the same epilogue.
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_combine_vec(SpmmArgs a) {
+    constexpr int GPB = kBlock / LPR;
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    const int64_t s = int64_t(blockIdx.x) * GPB + g;
+    if (s >= a.n_splits) return;
+    const lgcn_split_t sp = a.splits[s];
+    const int64_t d4 = int64_t(LPR) * NV;
+    const float4* p = reinterpret_cast<const float4*>(a.partial) + int64_t(sp.pbeg) * d4;
+    float4 acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int c = 0; c < sp.pcnt; ++c)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], p[int64_t(c) * d4 + l + k * LPR]);
+    finish_row_vec<LPR, NV>(a, sp.row, l, acc);
+}
+
+// ---- generic path: any d <= 64*KMAX, one wave per item, scalar columns ----
+constexpr int KMAX = 16;
+
+__device__ __forceinline__ void finish_row_scalar(const SpmmArgs& a, int64_t r, int l, const float (&v)[KMAX]) {
+    float* acc = split_row(a.acc_lo, a.acc_hi, a.acc_split, r, a.d);
+    const float* e = (a.mode == LGCN_EPI_INIT || a.mode == LGCN_EPI_FINAL_E)
+                         ? split_row(a.e_lo, a.e_hi, a.e_split, r, a.d)
+                         : nullptr;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int cidx = l + 64 * k;
+        if (cidx < a.d) {
+            float s;
+            if (a.mode == LGCN_EPI_STORE) s = v[k];
+            else if (e) s = e[cidx] + v[k];
+            else s = acc[cidx] + v[k];
+            if (a.mode == LGCN_EPI_FINAL_ACC || a.mode == LGCN_EPI_FINAL_E) s = (s / a.div) * a.mul;
+            acc[cidx] = s;
+            if (a.y != nullptr && (a.mode == LGCN_EPI_INIT || a.mode == LGCN_EPI_ADD))
+                a.y[r * a.d + cidx] = v[k];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_spmm_scalar(SpmmArgs a) {
+    const int g = threadIdx.x / 64;
+    const int l = threadIdx.x % 64;
+    const int64_t item = int64_t(blockIdx.x) * (kBlock / 64) + g;
+    if (item >= a.n_items) return;
+    const lgcn_item_t it = a.items[item];
+    float acc[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) acc[k] = 0.f;
+    for (int e = 0; e < it.len; ++e) {
+        const int cj = a.col[it.beg + e];
+        const float w = a.val[it.beg + e];
+        const float* src = split_row(a.x_lo, a.x_hi, a.x_split, int64_t(cj), a.d);
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int cidx = l + 64 * k;
+            if (cidx < a.d) acc[k] = acc[k] + w * src[cidx];
+        }
+    }
+    if (it.dst < 0) {
+        float* p = a.partial + int64_t(-it.dst - 1) * a.d;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k)
+            if (l + 64 * k < a.d) p[l + 64 * k] = acc[k];
+        return;
+    }
+    finish_row_scalar(a, it.dst, l, acc);
+}
+
+__global__ __launch_bounds__(kBlock) void k_combine_scalar(SpmmArgs a) {
+    const int g = threadIdx.x / 64;
+    const int l = threadIdx.x % 64;
+    const int64_t s = int64_t(blockIdx.x) * (kBlock / 64) + g;
+    if (s >= a.n_splits) return;
+    const lgcn_split_t sp = a.splits[s];
+    float acc[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) acc[k] = 0.f;
+    for (int c = 0; c < sp.pcnt; ++c) {
+        const float* p = a.partial + int64_t(sp.pbeg + c) * a.d;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k)
+            if (l + 64 * k < a.d) acc[k] = acc[k] + p[l + 64 * k];
+    }
+    finish_row_scalar(a, sp.row, l, acc);
+}
+
+enum { PASS_ITEMS = 1, PASS_COMBINE = 2, PASS_BOTH = 3 };
+
+template <int LPR, int NV, int UNROLL>
+int launch_vec(const SpmmArgs& a, hipStream_t s, int pass) {
+    constexpr int GPB = kBlock / LPR;
+    if ((pass & PASS_ITEMS) && a.n_items > 0) {
+        const int64_t blocks = (a.n_items + GPB - 1) / GPB;
+        k_spmm_vec<LPR, NV, UNROLL><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+        if (int rc = check_launch("k_spmm_vec")) return rc;
+    }
+    if ((pass & PASS_COMBINE) && a.n_splits > 0) {
+        const int64_t blocks = (a.n_splits + GPB - 1) / GPB;
+        k_combine_vec<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+        if (int rc = check_launch("k_combine_vec")) return rc;
+    }
+    return LGCN_OK;
+}
+
+int launch_scalar(const SpmmArgs& a, hipStream_t s, int pass) {
+    constexpr int GPB = kBlock / 64;
+    if ((pass & PASS_ITEMS) && a.n_items > 0) {
+        const int64_t blocks = (a.n_items + GPB - 1) / GPB;
+        k_spmm_scalar<<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+        if (int rc = check_launch("k_spmm_scalar")) return rc;
+    }
+    if ((pass & PASS_COMBINE) && a.n_splits > 0) {
+        const int64_t blocks = (a.n_splits + GPB - 1) / GPB;
+        k_combine_scalar<<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+        if (int rc = check_launch("k_combine_scalar")) return rc;
+    }
+    return LGCN_OK;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+__global__ void k_scale(const float* __restrict__ in, float* __restrict__ out, int64_t n, float mul, float div) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = (in[i] * mul) / div;
+}
+
+__global__ void k_copy_scale(const float* __restrict__ lo, const float* __restrict__ hi, int64_t split,
+                             int64_t N, int32_t d, float* __restrict__ out, float div, float mul) {
+    const int64_t n = N * d;
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t r = i / d;
+        const int64_t c = i - r * d;
+        const float x = (r < split) ? lo[r * d + c] : hi[(r - split) * d + c];
+        out[i] = (x / div) * mul;
+    }
+}
+
+int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* splits, int64_t n_splits,
+              const int32_t* col, const float* val, int64_t N, int32_t d, const float* x_lo,
+              const float* x_hi, int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split,
+              float* y, float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
+              float div, float mul, lgcn_stream_t stream, int pass) {
+    if (N < 0 || d <= 0 || n_items < 0 || n_splits < 0)
+        return fail(LGCN_E_ARG, "lgcn_spmm: bad sizes (N=%lld d=%d)", (long long)N, d);
+    if (mode < LGCN_EPI_INIT || mode > LGCN_EPI_STORE) return fail(LGCN_E_ARG, "lgcn_spmm: bad mode %d", mode);
+    if (N == 0 || n_items == 0) return LGCN_OK;
+    if (!items || !col || !val || !x_lo || !acc_lo)
+        return fail(LGCN_E_ARG, "lgcn_spmm: null items/col/val/x/acc");
+    if (x_split < N && !x_hi) return fail(LGCN_E_ARG, "lgcn_spmm: x_hi required (x_split < N)");
+    if (acc_split < N && !acc_hi) return fail(LGCN_E_ARG, "lgcn_spmm: acc_hi required (acc_split < N)");
+    const bool needs_e = (mode == LGCN_EPI_INIT || mode == LGCN_EPI_FINAL_E);
+    if (needs_e && (!e_lo || (e_split < N && !e_hi)))
+        return fail(LGCN_E_ARG, "lgcn_spmm: mode %d needs the e table", mode);
+    if (n_splits > 0 && (!splits || !partial)) return fail(LGCN_E_ARG, "lgcn_spmm: splits need partial scratch");
+    if (d > 64 * KMAX && d % 4 != 0)
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm: d=%d unsupported (d > %d needs d %% 4 == 0)", d, 64 * KMAX);
+
+    SpmmArgs a{items, n_items, splits, n_splits, col, val, x_lo, x_hi, x_split, e_lo, e_hi, e_split,
+               y, acc_lo, acc_hi, acc_split, partial, d, mode, div, mul};
+    hipStream_t s = as_stream(stream);
+
+    bool vec_ok = (d % 4 == 0) && aligned16(x_lo) && aligned16(acc_lo) && aligned16(partial) &&
+                  (x_hi == nullptr || aligned16(x_hi)) && (acc_hi == nullptr || aligned16(acc_hi)) &&
+                  (e_lo == nullptr || aligned16(e_lo)) && (e_hi == nullptr || aligned16(e_hi)) &&
+                  (y == nullptr || aligned16(y));
+    if (vec_ok) {
+        switch (d) {
+            case 4: return launch_vec<1, 1, 8>(a, s, pass);
+            case 8: return launch_vec<2, 1, 8>(a, s, pass);
+            case 16: return launch_vec<4, 1, 8>(a, s, pass);
+            case 32: return launch_vec<8, 1, 8>(a, s, pass);
+            case 64: return launch_vec<16, 1, 8>(a, s, pass);
+            case 128: return launch_vec<32, 1, 8>(a, s, pass);
+            case 256: return launch_vec<64, 1, 8>(a, s, pass);
+            case 512: return launch_vec<64, 2, 4>(a, s, pass);
+            case 1024: return launch_vec<64, 4, 2>(a, s, pass);
+            default: break;
+        }
+    }
+    if (d > 64 * KMAX) return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm: d=%d unsupported", d);
+    return launch_scalar(a, s, pass);
+}
+
+}  // namespace
+
+extern "C" {
+
+#define LGCN_SPMM_PARAMS                                                                             \
+    const lgcn_item_t *items, int64_t n_items, const lgcn_split_t *splits, int64_t n_splits,        \
+        const int32_t *col, const float *val, int64_t N, int32_t d, const float *x_lo,              \
+        const float *x_hi, int64_t x_split, const float *e_lo, const float *e_hi, int64_t e_split,  \
+        float *y, float *acc_lo, float *acc_hi, int64_t acc_split, float *partial, int32_t mode,     \
+        float div, float mul, lgcn_stream_t stream
+#define LGCN_SPMM_ARGS                                                                              \
+    items, n_items, splits, n_splits, col, val, N, d, x_lo, x_hi, x_split, e_lo, e_hi, e_split, y, \
+        acc_lo, acc_hi, acc_split, partial, mode, div, mul, stream
+
+int lgcn_spmm(LGCN_SPMM_PARAMS) { return spmm_impl(LGCN_SPMM_ARGS, PASS_BOTH); }
+int lgcn_spmm_items(LGCN_SPMM_PARAMS) { return spmm_impl(LGCN_SPMM_ARGS, PASS_ITEMS); }
+int lgcn_spmm_combine(LGCN_SPMM_PARAMS) { return spmm_impl(LGCN_SPMM_ARGS, PASS_COMBINE); }
+
+int lgcn_scale(const float* in, float* out, int64_t n, float mul, float div, lgcn_stream_t stream) {
+    if (n < 0 || (n > 0 && (!in || !out))) return fail(LGCN_E_ARG, "lgcn_scale: bad args");
+    if (n == 0) return LGCN_OK;
+    k_scale<<<grid_for(n, kBlock, 16384), kBlock, 0, as_stream(stream)>>>(in, out, n, mul, div);
+    return check_launch("k_scale");
+}
+
+int lgcn_copy_scale(const float* x_lo, const float* x_hi, int64_t x_split, int64_t N, int32_t d,
+                    float* out, float div, float mul, lgcn_stream_t stream) {
+    if (N < 0 || d <= 0 || (N > 0 && (!x_lo || !out)) || (x_split < N && !x_hi))
+        return fail(LGCN_E_ARG, "lgcn_copy_scale: bad args");
+    if (N == 0) return LGCN_OK;
+    k_copy_scale<<<grid_for(N * d, kBlock, 16384), kBlock, 0, as_stream(stream)>>>(x_lo, x_hi, x_split, N, d,
+                                                                                   out, div, mul);
+    return check_launch("k_copy_scale");
+}
+
+}  // extern "C"

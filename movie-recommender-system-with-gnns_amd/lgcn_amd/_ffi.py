@@ -1,0 +1,104 @@
+"""ctypes binding of liblgcn.so (the C ABI in include/lgcn.h).
+
+This is the whole Python↔native boundary: plain pointers (``tensor.data_ptr()``), sizes and
+the caller's HIP stream (``torch.cuda.current_stream().cuda_stream``). No torch types cross it.
+The product path has no CPU fallback: if the library is missing, or no ROCm device is present,
+every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import pathlib
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = _HERE / "liblgcn.so"
+
+EPI_INIT = 0
+EPI_ADD = 1
+EPI_FINAL_ACC = 2
+EPI_FINAL_E = 3
+EPI_STORE = 4
+
+ITEM_BYTES = 16   # lgcn_item_t {int64 beg; int32 len; int32 dst}
+SPLIT_BYTES = 16  # lgcn_split_t {int32 row, pbeg, pcnt, pad}
+
+_lib = None
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_f32 = ctypes.c_float
+_sz = ctypes.c_size_t
+
+_SIGS = {
+    "lgcn_last_error": ([], ctypes.c_char_p),
+    "lgcn_abi_version": ([], ctypes.c_int),
+    "lgcn_csr_workspace_size": ([_i64, _i64, ctypes.POINTER(_sz)], ctypes.c_int),
+    "lgcn_csr_build": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
+    "lgcn_inv_sqrt_degree": ([_vp, _i64, _vp, _vp], ctypes.c_int),
+    "lgcn_edge_norm": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp], ctypes.c_int),
+    "lgcn_schedule_workspace_size": ([_i64, _i64, _i32, ctypes.POINTER(_sz)], ctypes.c_int),
+    "lgcn_schedule_build": ([_vp, _i64, _i64, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _sz, _vp], ctypes.c_int),
+    "lgcn_spmm": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
+                   _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp],
+                  ctypes.c_int),
+    "lgcn_spmm_items": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
+                         _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp],
+                        ctypes.c_int),
+    "lgcn_spmm_combine": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
+                           _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp],
+                          ctypes.c_int),
+    "lgcn_scale": ([_vp, _vp, _i64, _f32, _f32, _vp], ctypes.c_int),
+    "lgcn_copy_scale": ([_vp, _vp, _i64, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+class LgcnError(RuntimeError):
+    pass
+
+
+def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
+    """Load liblgcn.so (does not touch the GPU). Raises if it has not been built."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = pathlib.Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise LgcnError(f"{p} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                        " (the MI355X path has no CPU fallback)")
+    lib = ctypes.CDLL(str(p))
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    if lib.lgcn_abi_version() != 1:
+        raise LgcnError(f"liblgcn ABI version {lib.lgcn_abi_version()} != 1")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().lgcn_last_error().decode(errors="replace")
+        raise LgcnError(f"{what} failed (rc={rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """data_ptr of a tensor (None for None)."""
+    return None if t is None else t.data_ptr()
+
+
+def require_device(t, what: str) -> None:
+    if not t.is_cuda:
+        raise LgcnError(f"{what}: the MI355X LightGCN path needs ROCm device tensors, got {t.device}"
+                        " (move the model and edge_index to 'cuda'; there is no CPU fallback)")
+
+
+def stream_of(device) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,163 @@
+"""Propagation plans: the device-resident CSR + gcn_norm weights + load-balanced schedule that
+one ``edge_index`` needs, built once and reused by every layer and every step.
+
+The reference re-derives all of this inside every LGConv call (PyG 2.4.0 ``gcn_norm`` +
+``propagate``, reached from reference models/light_gcn.py:33), K times per forward; the
+result is identical each time, so a plan per edge set is a legal cache.
+
+HBM layout of one direction (``CsrDirection``), E edges, N nodes:
+    rowptr int64[N+1] | col int32[E] | val fp32[E] | eid int32[E] (edge position, tests/debug)
+    items  lgcn_item_t[cap] (16 B)    | splits lgcn_split_t[N] (16 B)
+The forward direction has rows = targets (edge_index[1]); the transposed direction (built
+lazily, only when autograd needs it) has rows = sources (edge_index[0]). Both keep the input
+edge order inside a row, which is the order CPU scatter_add_/index_add_ add in.
+"""
+from __future__ import annotations
+
+import dataclasses
+import weakref
+
+import torch
+
+from . import _ffi
+
+DEFAULT_CHUNK = 256
+
+
+@dataclasses.dataclass
+class CsrDirection:
+    rowptr: torch.Tensor
+    col: torch.Tensor
+    eid: torch.Tensor
+    val: torch.Tensor
+    items: torch.Tensor   # int64 [cap, 2] viewed as lgcn_item_t
+    splits: torch.Tensor  # int32 [N, 4] viewed as lgcn_split_t
+    n_items: int
+    n_splits: int
+    n_partials: int
+    chunk: int
+
+    def item_table(self) -> torch.Tensor:
+        """Items as int64 [n_items, 3] = (beg, len, dst) — for tests."""
+        it = self.items[: self.n_items]
+        lens_dst = it[:, 1].view(torch.int32).view(-1, 2)
+        return torch.stack([it[:, 0], lens_dst[:, 0].long(), lens_dst[:, 1].long()], dim=1)
+
+
+def _build_direction(key: torch.Tensor, other: torch.Tensor, N: int, chunk: int,
+                     dis: torch.Tensor | None, stream: int) -> tuple[CsrDirection, torch.Tensor, int]:
+    lib = _ffi.load()
+    dev = key.device
+    E = key.numel()
+    bytes_ = _ffi._sz(0)
+    _ffi.check(lib.lgcn_csr_workspace_size(E, N, bytes_), "lgcn_csr_workspace_size")
+    ws = torch.empty(max(1, bytes_.value), dtype=torch.uint8, device=dev)
+    rowptr = torch.empty(N + 1, dtype=torch.int64, device=dev)
+    col = torch.empty(E, dtype=torch.int32, device=dev)
+    eid = torch.empty(E, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int64, device=dev)
+    _ffi.check(lib.lgcn_csr_build(_ffi.ptr(key), _ffi.ptr(other), E, N, rowptr.data_ptr(), col.data_ptr(),
+                                  eid.data_ptr(), err.data_ptr(), ws.data_ptr(), ws.numel(), stream),
+               "lgcn_csr_build")
+    if dis is None:
+        dis = torch.empty(N, dtype=torch.float32, device=dev)
+        _ffi.check(lib.lgcn_inv_sqrt_degree(rowptr.data_ptr(), N, dis.data_ptr(), stream), "lgcn_inv_sqrt_degree")
+    val = torch.empty(E, dtype=torch.float32, device=dev)
+    _ffi.check(lib.lgcn_edge_norm(rowptr.data_ptr(), col.data_ptr(), N, E, dis.data_ptr(), val.data_ptr(), stream),
+               "lgcn_edge_norm")
+
+    _ffi.check(lib.lgcn_schedule_workspace_size(E, N, chunk, bytes_), "lgcn_schedule_workspace_size")
+    ws2 = torch.empty(max(1, bytes_.value), dtype=torch.uint8, device=dev)
+    cap = N + E // chunk + 1
+    items = torch.empty((cap, 2), dtype=torch.int64, device=dev)
+    splits = torch.empty((max(N, 1), 4), dtype=torch.int32, device=dev)
+    counts = torch.zeros(3, dtype=torch.int64, device=dev)
+    _ffi.check(lib.lgcn_schedule_build(rowptr.data_ptr(), N, E, chunk, items.data_ptr(), cap, splits.data_ptr(),
+                                       splits.shape[0], counts.data_ptr(), ws2.data_ptr(), ws2.numel(), stream),
+               "lgcn_schedule_build")
+    # one host read-back per plan: ids check + schedule sizes (the launches need them)
+    host = torch.cat([counts, err]).cpu()
+    n_items, n_splits, n_partials, n_bad = (int(v) for v in host.tolist())
+    del ws, ws2
+    return CsrDirection(rowptr, col, eid, val, items, splits, n_items, n_splits, n_partials, chunk), dis, n_bad
+
+
+class PropagationPlan:
+    """Forward (+ lazily transposed) plan for one edge set over N = num_users + num_items nodes."""
+
+    def __init__(self, edge_index: torch.Tensor, num_nodes: int, chunk: int = DEFAULT_CHUNK):
+        _ffi.require_device(edge_index, "PropagationPlan")
+        if edge_index.dim() != 2 or edge_index.shape[0] != 2:
+            raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
+        if edge_index.dtype != torch.int64:
+            raise TypeError(f"edge_index must be int64 (torch.long), got {edge_index.dtype}")
+        self.num_nodes = int(num_nodes)
+        self.num_edges = int(edge_index.shape[1])
+        self.chunk = int(chunk)
+        self.device = edge_index.device
+        self._src = edge_index[0].contiguous()
+        self._dst = edge_index[1].contiguous()
+        stream = _ffi.stream_of(self.device)
+        # forward: rows = targets (PyG flow source_to_target aggregates at edge_index[1])
+        self.fwd, self.dis, bad = _build_direction(self._dst, self._src, self.num_nodes, self.chunk, None, stream)
+        if bad:
+            raise IndexError(f"edge_index holds {bad} edge(s) with a node id outside [0, {self.num_nodes})")
+        self._bwd: CsrDirection | None = None
+
+    @property
+    def bwd(self) -> CsrDirection:
+        """Transposed plan (rows = sources) for the autograd backward; weights reuse the
+        forward in-degree normalisation, so val_T[q] == val[edge] exactly."""
+        if self._bwd is None:
+            stream = _ffi.stream_of(self.device)
+            self._bwd, _, _ = _build_direction(self._src, self._dst, self.num_nodes, self.chunk, self.dis, stream)
+        return self._bwd
+
+    def nbytes(self) -> int:
+        tot = 0
+        for d in (self.fwd, self._bwd):
+            if d is None:
+                continue
+            for t in (d.rowptr, d.col, d.eid, d.val, d.items, d.splits):
+                tot += t.numel() * t.element_size()
+        return tot + self.dis.numel() * 4
+
+
+class PlanCache:
+    """Plans keyed by the edge_index tensor object (weakly referenced) and its version counter:
+    a tensor that is modified in place or freed never hits a stale plan."""
+
+    def __init__(self, max_entries: int = 4096, chunk: int = DEFAULT_CHUNK):
+        self.max_entries = max_entries
+        self.chunk = chunk
+        self._entries: dict[tuple, tuple[weakref.ref, PropagationPlan]] = {}
+
+    def get(self, edge_index: torch.Tensor, num_nodes: int) -> PropagationPlan:
+        key = (id(edge_index), edge_index.data_ptr(), tuple(edge_index.shape), tuple(edge_index.stride()),
+               edge_index._version, int(num_nodes), str(edge_index.device))
+        hit = self._entries.get(key)
+        if hit is not None:
+            ref, plan = hit
+            if ref() is edge_index:
+                # LRU refresh
+                self._entries.pop(key)
+                self._entries[key] = hit
+                return plan
+            self._entries.pop(key)
+        plan = PropagationPlan(edge_index, num_nodes, self.chunk)
+        self._entries[key] = (weakref.ref(edge_index), plan)
+        self._evict()
+        return plan
+
+    def _evict(self) -> None:
+        dead = [k for k, (r, _) in self._entries.items() if r() is None]
+        for k in dead:
+            self._entries.pop(k)
+        while len(self._entries) > self.max_entries:
+            self._entries.pop(next(iter(self._entries)))
+
+    def clear(self) -> None:
+        self._entries.clear()
+
+    def __len__(self) -> int:
+        return len(self._entries)

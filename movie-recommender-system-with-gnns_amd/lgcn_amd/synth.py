@@ -1,0 +1,89 @@
+"""Synthetic MovieLens-shaped bipartite graphs (no dataset exists offline).
+
+The reference builds its graph from MovieLens-25M ratings >= 4 (reference
+data/dataset_handler.py:105-141): users are ids [0, U), movies [U, U+I), and
+``to_undirected`` makes both directions and coalesces (sorted by row*N+col, deduplicated).
+``ml25m_shaped`` produces the same structure from seeded Zipf-like user activity and item
+popularity, calibrated to ML-25M's scale (U=162,541, I=59,047, ~12.45M unique rating>=4 pairs,
+E ≈ 2.49e7 directed edges) and skew (hub items with 1e4–1e5 raters, medians of tens).
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+ML25M_USERS = 162_541
+ML25M_ITEMS = 59_047
+ML25M_PAIRS = 12_450_000
+
+
+@dataclasses.dataclass
+class BipartiteGraph:
+    num_users: int
+    num_items: int
+    edge_index: np.ndarray  # int64 [2, E], coalesced undirected (users first)
+
+    @property
+    def num_nodes(self) -> int:
+        return self.num_users + self.num_items
+
+    @property
+    def num_edges(self) -> int:
+        return int(self.edge_index.shape[1])
+
+    def degree_stats(self) -> dict:
+        deg = np.bincount(self.edge_index[1], minlength=self.num_nodes)
+        du, di = deg[: self.num_users], deg[self.num_users:]
+        return {"user_max": int(du.max()), "user_median": float(np.median(du)),
+                "item_max": int(di.max()), "item_median": float(np.median(di))}
+
+
+def zipf_weights(n: int, alpha: float, offset: float, rng: np.random.Generator) -> np.ndarray:
+    w = 1.0 / np.power(np.arange(1, n + 1, dtype=np.float64) + offset, alpha)
+    w = w[rng.permutation(n)]  # hubs at random ids, as in real id maps
+    return w / w.sum()
+
+
+def undirected_from_pairs(users: np.ndarray, items: np.ndarray, num_users: int, num_items: int) -> np.ndarray:
+    """Coalesced undirected edge_index of user–item pairs (reference data/dataset_handler.py:139-141)."""
+    N = num_users + num_items
+    u = users.astype(np.int64)
+    i = items.astype(np.int64) + num_users
+    key = np.concatenate([u * N + i, i * N + u])
+    key = np.unique(key)
+    return np.stack([key // N, key % N])
+
+
+def random_pairs(num_users: int, num_items: int, num_pairs: int, seed: int = 0, user_alpha: float = 0.75,
+                 user_offset: float = 40.0, item_alpha: float = 1.0, item_offset: float = 12.0):
+    rng = np.random.default_rng(seed)
+    max_pairs = num_users * num_items
+    num_pairs = min(num_pairs, max_pairs)
+    pu = zipf_weights(num_users, user_alpha, user_offset, rng)
+    pi = zipf_weights(num_items, item_alpha, item_offset, rng)
+    keys = np.empty(0, dtype=np.int64)
+    draw = int(num_pairs * 1.25) + 16
+    for _ in range(12):
+        u = rng.choice(num_users, size=draw, p=pu)
+        it = rng.choice(num_items, size=draw, p=pi)
+        keys = np.unique(np.concatenate([keys, u.astype(np.int64) * num_items + it]))
+        if keys.size >= num_pairs:
+            break
+        draw = int((num_pairs - keys.size) * 2.0) + 1024
+    if keys.size > num_pairs:
+        keys = np.sort(rng.choice(keys, size=num_pairs, replace=False))
+    return keys // num_items, keys % num_items
+
+
+def bipartite(num_users: int, num_items: int, num_pairs: int, seed: int = 0, **kw) -> BipartiteGraph:
+    u, i = random_pairs(num_users, num_items, num_pairs, seed, **kw)
+    return BipartiteGraph(num_users, num_items, undirected_from_pairs(u, i, num_users, num_items))
+
+
+def ml25m_shaped(seed: int = 0, scale: float = 1.0) -> BipartiteGraph:
+    """The C2 graph (scale=1): ML-25M-shaped, E ≈ 2.49e7 directed edges."""
+    U = max(2, int(ML25M_USERS * scale))
+    I = max(2, int(ML25M_ITEMS * scale))
+    P = max(1, int(ML25M_PAIRS * scale))
+    return bipartite(U, I, P, seed)

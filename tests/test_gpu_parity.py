@@ -1,0 +1,216 @@
+"""HIP path vs the CPU oracle, through the C ABI (lgcn_amd → liblgcn.so).
+
+Bars (BASELINE.json north_star): CSR index construction bit-exact; propagation within 1e-5
+relative fp32. With every row unsplit (chunk >= max degree) the kernels add in exactly the
+oracle's order, so forward and backward are also checked bit for bit.
+"""
+import numpy as np
+import pytest
+import torch
+
+import graphs
+from oracle import c_oracle
+from oracle import lgconv_ref as R
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5  # relative to max |reference|, per the north star
+
+
+def rel_err(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)) if b.size else 0.0
+
+
+def _plan(ei, N, dev, chunk=None):
+    from lgcn_amd.plan import DEFAULT_CHUNK, PropagationPlan
+
+    return PropagationPlan(torch.from_numpy(ei).to(dev), N, chunk or DEFAULT_CHUNK)
+
+
+@pytest.mark.parametrize("name", list(graphs.ALL))
+def test_csr_bit_exact(gpu, name):
+    U, I, ei = graphs.ALL[name]()
+    N = U + I
+    plan = _plan(ei, N, gpu)
+    for direction, key, other in ((plan.fwd, ei[1], ei[0]), (plan.bwd, ei[0], ei[1])):
+        rp, col, eid = c_oracle.csr_build(key, other, N)
+        assert np.array_equal(direction.rowptr.cpu().numpy(), rp)
+        assert np.array_equal(direction.col.cpu().numpy(), col)
+        assert np.array_equal(direction.eid.cpu().numpy(), eid)
+    # gcn_norm weights, bit-exact, in CSR order
+    dis, w_edge = c_oracle.gcn_norm(ei, N)
+    assert np.array_equal(plan.dis.cpu().numpy(), dis)
+    assert np.array_equal(plan.fwd.val.cpu().numpy(), w_edge[plan.fwd.eid.cpu().numpy()])
+    assert np.array_equal(plan.bwd.val.cpu().numpy(), w_edge[plan.bwd.eid.cpu().numpy()])
+
+
+@pytest.mark.parametrize("chunk", [1, 3, 16, 256])
+def test_schedule_covers_rows(gpu, chunk):
+    U, I, ei = graphs.hub()
+    N = U + I
+    plan = _plan(ei, N, gpu, chunk)
+    f = plan.fwd
+    items = f.item_table().cpu().numpy()
+    rowptr = f.rowptr.cpu().numpy()
+    deg = np.diff(rowptr)
+    assert f.n_items == sum(max(1, -(-int(x) // chunk)) for x in deg)
+    # longest first
+    assert np.all(np.diff(items[:, 1]) <= 0)
+    covered = np.zeros(rowptr[-1], np.int64)
+    whole_rows = items[items[:, 2] >= 0, 2]
+    assert len(set(whole_rows.tolist())) == len(whole_rows)
+    for beg, ln, dst in items:
+        covered[beg:beg + ln] += 1
+        assert ln <= chunk
+    assert np.all(covered == 1)
+    splits = f.splits[: f.n_splits].cpu().numpy()
+    assert set(whole_rows.tolist()) | set(splits[:, 0].tolist()) == set(range(N))
+    assert f.n_partials == int(splits[:, 2].sum()) if f.n_splits else f.n_partials == 0
+
+
+@pytest.mark.parametrize("name", list(graphs.ALL))
+@pytest.mark.parametrize("K", [0, 1, 2, 3, 4])
+def test_forward_backward(gpu, name, K):
+    from models.light_gcn import LightGCN
+
+    U, I, ei = graphs.ALL[name]()
+    d = 64
+    uw, iw = graphs.embeddings(U, I, d, seed=K)
+    model = LightGCN(U, I, num_layers=K, dim_h=d).to(gpu)
+    with torch.no_grad():
+        model.user_embedding.weight.copy_(torch.from_numpy(uw))
+        model.item_embedding.weight.copy_(torch.from_numpy(iw))
+    et = torch.from_numpy(ei).to(gpu)
+    users, items = model(et)
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
+    assert users.shape == (U, d) and items.shape == (I, d)
+    assert rel_err(users.detach().cpu().numpy(), ru) <= RTOL
+    assert rel_err(items.detach().cpu().numpy(), ri) <= RTOL
+
+    dF = np.random.default_rng(K + 11).standard_normal((U + I, d)).astype(np.float32)
+    (torch.cat([users, items]) * torch.from_numpy(dF).to(gpu)).sum().backward()
+    gu, gi = c_oracle.lightgcn_backward(dF, ei, U, K)
+    assert rel_err(model.user_embedding.weight.grad.cpu().numpy(), gu) <= RTOL
+    assert rel_err(model.item_embedding.weight.grad.cpu().numpy(), gi) <= RTOL
+
+
+@pytest.mark.parametrize("name", ["sym", "subsampled", "shuffled", "hub"])
+def test_bit_exact_unsplit(gpu, name):
+    """chunk >= max degree: every row is one item, summed in CSR order with mul-then-add —
+    bitwise the reference CPU scatter_add_ result, forward and backward."""
+    from lgcn_amd import propagate_backward, propagate_forward
+
+    U, I, ei = graphs.ALL[name]()
+    N, K, d = U + I, 3, 64
+    plan = _plan(ei, N, gpu, chunk=1 << 20)
+    assert plan.fwd.n_splits == 0
+    uw, iw = graphs.embeddings(U, I, d, seed=5)
+    out = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, K)
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
+    assert np.array_equal(out.cpu().numpy(), np.concatenate([ru, ri]))
+    dF = np.random.default_rng(3).standard_normal((N, d)).astype(np.float32)
+    gu, gi = propagate_backward(torch.from_numpy(dF).to(gpu), plan, U, K)
+    ou, oi = c_oracle.lightgcn_backward(dF, ei, U, K)
+    assert np.array_equal(gu.cpu().numpy(), ou)
+    assert np.array_equal(gi.cpu().numpy(), oi)
+
+
+@pytest.mark.parametrize("d", [3, 4, 8, 16, 32, 96, 128, 256, 512, 200])
+def test_widths(gpu, d):
+    """Vector kernels (d in {4..1024} powers of two) and the scalar path (other d)."""
+    from lgcn_amd import propagate_backward, propagate_forward
+
+    U, I, ei = graphs.hub(U=600, I=40)
+    N, K = U + I, 2
+    plan = _plan(ei, N, gpu, chunk=64)
+    uw, iw = graphs.embeddings(U, I, d, seed=d)
+    out = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, K)
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
+    assert rel_err(out.cpu().numpy(), np.concatenate([ru, ri])) <= RTOL
+    dF = np.random.default_rng(d).standard_normal((N, d)).astype(np.float32)
+    gu, gi = propagate_backward(torch.from_numpy(dF).to(gpu), plan, U, K)
+    ou, oi = c_oracle.lightgcn_backward(dF, ei, U, K)
+    assert rel_err(np.concatenate([gu.cpu().numpy(), gi.cpu().numpy()]), np.concatenate([ou, oi])) <= RTOL
+
+
+def test_lgconv_operator(gpu):
+    """The single-layer operator boundary: LGConv()(x, edge_index) and its gradient."""
+    import lgcn_amd
+
+    U, I, ei = graphs.subsampled()
+    N, d = U + I, 64
+    x = np.random.default_rng(0).standard_normal((N, d)).astype(np.float32)
+    xt = torch.from_numpy(x).to(gpu).requires_grad_(True)
+    conv = lgcn_amd.LGConv()
+    y = conv(x=xt, edge_index=torch.from_numpy(ei).to(gpu))
+    w = R.gcn_norm(ei, N)
+    assert rel_err(y.detach().cpu().numpy(), R.lgconv(x, ei, w)) <= RTOL
+    dy = np.random.default_rng(1).standard_normal((N, d)).astype(np.float32)
+    y.backward(torch.from_numpy(dy).to(gpu))
+    assert rel_err(xt.grad.cpu().numpy(), R.lgconv_transposed(dy, ei, w)) <= RTOL
+
+
+def test_empty_edges(gpu):
+    from models.light_gcn import LightGCN
+
+    U, I, d, K = 7, 5, 64, 3
+    model = LightGCN(U, I, num_layers=K, dim_h=d).to(gpu)
+    ei = torch.empty((2, 0), dtype=torch.int64, device=gpu)
+    users, items = model(ei)
+    uw = model.user_embedding.weight.detach().cpu().numpy()
+    iw = model.item_embedding.weight.detach().cpu().numpy()
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, np.zeros((2, 0), np.int64), K)
+    assert np.array_equal(users.detach().cpu().numpy(), ru)
+    assert np.array_equal(items.detach().cpu().numpy(), ri)
+    (users.sum() + items.sum()).backward()
+    assert torch.all(model.user_embedding.weight.grad == (1.0 * np.float32(0.25)) / 4)
+
+
+def test_out_of_range_ids_raise(gpu):
+    from models.light_gcn import LightGCN
+
+    model = LightGCN(4, 3, num_layers=2, dim_h=8).to(gpu)
+    bad = torch.tensor([[0, 1], [4, 7]], dtype=torch.int64, device=gpu)  # 7 >= N
+    with pytest.raises(IndexError):
+        model(bad)
+
+
+def test_deterministic(gpu):
+    from lgcn_amd import propagate_forward
+
+    U, I, ei = graphs.hub()
+    plan = _plan(ei, U + I, gpu, chunk=32)
+    uw, iw = graphs.embeddings(U, I, 64)
+    a = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, 3)
+    b = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, 3)
+    assert torch.equal(a, b)
+
+
+def test_plan_cache_reuse_and_invalidation(gpu):
+    from models.light_gcn import LightGCN
+
+    U, I, ei = graphs.sym()
+    model = LightGCN(U, I, num_layers=2, dim_h=16).to(gpu)
+    et = torch.from_numpy(ei).to(gpu)
+    p1 = model.plan_for(et)
+    assert model.plan_for(et) is p1
+    et[0, 0] = et[0, 0]  # in-place write bumps the version counter
+    assert model.plan_for(et) is not p1
+
+
+def test_ml25m_scaled_parity(gpu):
+    """A 5%-scale ML-25M-shaped graph (E ≈ 1.2M) with the default schedule."""
+    from lgcn_amd import synth
+    from models.light_gcn import LightGCN
+
+    g = synth.ml25m_shaped(seed=3, scale=0.05)
+    U, I, K, d = g.num_users, g.num_items, 3, 64
+    model = LightGCN(U, I, num_layers=K, dim_h=d).to(gpu)
+    users, items = model(torch.from_numpy(g.edge_index).to(gpu))
+    uw = model.user_embedding.weight.detach().cpu().numpy()
+    iw = model.item_embedding.weight.detach().cpu().numpy()
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, g.edge_index, K)
+    assert rel_err(users.detach().cpu().numpy(), ru) <= RTOL
+    assert rel_err(items.detach().cpu().numpy(), ri) <= RTOL
