@@ -154,23 +154,47 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
     finish_row_vec<LPR, NV>(a, it.dst, l, acc);
 }
 
-// Split rows: add the chunk partials in chunk (= edge) order, then the same epilogue.
+// Split rows: one workgroup per split row. Group g (of GPB) sums partials g, g+GPB, g+2*GPB, ...
+// with UNROLL loads in flight; the GPB group sums are then added in group order through LDS.
+// The association is fixed by the code, so results are deterministic run to run.
 template <int LPR, int NV>
 __global__ __launch_bounds__(kBlock) void k_combine_vec(SpmmArgs a) {
     constexpr int GPB = kBlock / LPR;
+    constexpr int UNROLL = 4;
+    __shared__ float4 lds[GPB][LPR * NV];
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
-    const int64_t s = int64_t(blockIdx.x) * GPB + g;
-    if (s >= a.n_splits) return;
+    const int64_t s = blockIdx.x;
+    if (s >= a.n_splits) return;  // whole block
     const lgcn_split_t sp = a.splits[s];
     const int64_t d4 = int64_t(LPR) * NV;
     const float4* p = reinterpret_cast<const float4*>(a.partial) + int64_t(sp.pbeg) * d4;
     float4 acc[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int c = 0; c < sp.pcnt; ++c)
+    int c = g;
+    for (; c + (UNROLL - 1) * GPB < sp.pcnt; c += UNROLL * GPB) {
+        float4 t[UNROLL][NV];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) t[u][k] = p[int64_t(c + u * GPB) * d4 + l + k * LPR];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], t[u][k]);
+    }
+    for (; c < sp.pcnt; c += GPB)
 #pragma unroll
         for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], p[int64_t(c) * d4 + l + k * LPR]);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) lds[g][l + k * LPR] = acc[k];
+    __syncthreads();
+    if (g != 0) return;
+    const int ng = sp.pcnt < GPB ? sp.pcnt : GPB;
+    for (int h = 1; h < ng; ++h)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], lds[h][l + k * LPR]);
     finish_row_vec<LPR, NV>(a, sp.row, l, acc);
 }
 
@@ -256,8 +280,7 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass) {
         if (int rc = check_launch("k_spmm_vec")) return rc;
     }
     if ((pass & PASS_COMBINE) && a.n_splits > 0) {
-        const int64_t blocks = (a.n_splits + GPB - 1) / GPB;
-        k_combine_vec<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+        k_combine_vec<LPR, NV><<<dim3(static_cast<unsigned>(a.n_splits)), kBlock, 0, s>>>(a);
         if (int rc = check_launch("k_combine_vec")) return rc;
     }
     return LGCN_OK;
@@ -307,8 +330,8 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
         return fail(LGCN_E_ARG, "lgcn_spmm: bad sizes (N=%lld d=%d)", (long long)N, d);
     if (mode < LGCN_EPI_INIT || mode > LGCN_EPI_STORE) return fail(LGCN_E_ARG, "lgcn_spmm: bad mode %d", mode);
     if (N == 0 || n_items == 0) return LGCN_OK;
-    if (!items || !col || !val || !x_lo || !acc_lo)
-        return fail(LGCN_E_ARG, "lgcn_spmm: null items/col/val/x/acc");
+    // col/val may be NULL for an edge-free plan (every item then has len 0)
+    if (!items || !x_lo || !acc_lo) return fail(LGCN_E_ARG, "lgcn_spmm: null items/x/acc");
     if (x_split < N && !x_hi) return fail(LGCN_E_ARG, "lgcn_spmm: x_hi required (x_split < N)");
     if (acc_split < N && !acc_hi) return fail(LGCN_E_ARG, "lgcn_spmm: acc_hi required (acc_split < N)");
     const bool needs_e = (mode == LGCN_EPI_INIT || mode == LGCN_EPI_FINAL_E);

@@ -40,7 +40,7 @@ class CsrDirection:
     def item_table(self) -> torch.Tensor:
         """Items as int64 [n_items, 3] = (beg, len, dst) — for tests."""
         it = self.items[: self.n_items]
-        lens_dst = it[:, 1].view(torch.int32).view(-1, 2)
+        lens_dst = it[:, 1].contiguous().view(torch.int32).view(-1, 2)
         return torch.stack([it[:, 0], lens_dst[:, 0].long(), lens_dst[:, 1].long()], dim=1)
 
 
