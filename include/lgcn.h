@@ -177,6 +177,16 @@ int lgcn_scale(const float* in, float* out, int64_t n, float mul, float div, lgc
 int lgcn_copy_scale(const float* x_lo, const float* x_hi, int64_t x_split, int64_t N, int32_t d,
                     float* out, float div, float mul, lgcn_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Host-side (no GPU): balanced k-way node partition for Cluster-GCN batching, the METIS
+ * replacement for PyG ClusterData (reference data/dataset_handler.py:273). Deterministic
+ * restreaming Linear Deterministic Greedy over the undirected adjacency of (src[e], dst[e]);
+ * part_out[N] receives ids in [0, num_parts); `imbalance` is the streaming capacity slack and a
+ * final fix-up leaves every part with exactly floor or ceil(N/num_parts) nodes. Host pointers. Errors: lgcn_partition_last_error(). */
+int lgcn_partition_edges(const int64_t* src, const int64_t* dst, int64_t E, int64_t N,
+                         int32_t num_parts, int32_t passes, float imbalance, int32_t* part_out);
+const char* lgcn_partition_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

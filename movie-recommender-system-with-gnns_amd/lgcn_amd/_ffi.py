@@ -51,6 +51,8 @@ _SIGS = {
                           ctypes.c_int),
     "lgcn_scale": ([_vp, _vp, _i64, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_copy_scale": ([_vp, _vp, _i64, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),
+    "lgcn_partition_edges": ([_vp, _vp, _i64, _i64, _i32, _i32, _f32, _vp], ctypes.c_int),
+    "lgcn_partition_last_error": ([], ctypes.c_char_p),
 }
 
 EXPORTED = tuple(_SIGS)

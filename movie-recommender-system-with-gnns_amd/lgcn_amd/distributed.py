@@ -1,0 +1,75 @@
+"""Data-parallel Cluster-GCN training over one process per GPU (torch.distributed; backend
+"nccl" is RCCL over xGMI on MI355X, "gloo" on CPU for tests).
+
+The reference trains one Cluster-GCN part per step on one GPU (reference utils/train_test.py:
+66-103 over data/dataset_handler.py:285's loader). Here each of W ranks takes a disjoint batch of
+parts per step from an epoch permutation every rank derives from the same seed, runs forward +
+BPR + backward locally, then the two dense embedding gradients ([U,d] and [I,d]) are summed
+with one all_reduce each and divided by W, and every rank applies the identical
+clip_grad_norm_(1) + Adam step, so the replicated tables stay bitwise identical.
+With W = 1 this is exactly the reference step.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def world_info():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def epoch_order(num_batches: int, seed: int, epoch: int) -> torch.Tensor:
+    """The shared shuffled order of batches for one epoch (same on every rank)."""
+    g = torch.Generator().manual_seed(seed * 1_000_003 + epoch)
+    return torch.randperm(num_batches, generator=g)
+
+
+def rank_share(num_batches: int, world: int, rank: int, seed: int, epoch: int) -> list[int]:
+    """Rank r's batches for the epoch: order[r], order[r + W], ... — every rank gets the same number
+    of steps (the last num_batches % W batches of the order are left for the next epoch's shuffle)."""
+    order = epoch_order(num_batches, seed, epoch).tolist()
+    steps = num_batches // world
+    if steps == 0:
+        raise ValueError(f"{num_batches} batches cannot feed {world} ranks")
+    return [order[s * world + rank] for s in range(steps)]
+
+
+def allreduce_grads(params, world: int) -> None:
+    if world == 1:
+        return
+    for p in params:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+        dist.all_reduce(p.grad, op=dist.ReduceOp.SUM)
+        p.grad.div_(world)
+
+
+def train_epoch(model, optimizer, batches, device, seed: int = 0, epoch: int = 0, loss_fn=None,
+                embed_fn=None, max_norm: float = 1.0) -> float:
+    """One data-parallel epoch; returns the global edge-weighted mean loss (as reference train())."""
+    from utils.train_test import bpr_loss, compute_embeddings
+
+    loss_fn = loss_fn or bpr_loss
+    embed_fn = embed_fn or compute_embeddings
+    world, rank = world_info()
+    model.train()
+    params = list(model.parameters())
+    acc = torch.zeros(2, dtype=torch.float64, device=device)  # [sum loss*w, sum w]
+    for b in rank_share(len(batches), world, rank, seed, epoch):
+        batch = batches[b].to(device)
+        optimizer.zero_grad()
+        loss = loss_fn(*embed_fn(model, batch, device))
+        loss.backward()
+        allreduce_grads(params, world)
+        torch.nn.utils.clip_grad_norm_(params, max_norm=max_norm)
+        optimizer.step()
+        w = batch.edge_index.shape[1]
+        acc[0] += loss.detach().double() * w
+        acc[1] += w
+    if world > 1:
+        dist.all_reduce(acc, op=dist.ReduceOp.SUM)
+    tot = acc.cpu().tolist()
+    return tot[0] / tot[1]

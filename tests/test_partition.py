@@ -1,0 +1,68 @@
+"""Host partitioner (METIS replacement) and Cluster-GCN batching — no GPU needed."""
+import numpy as np
+import pytest
+
+from lgcn_amd import _ffi, cluster, synth
+
+
+def planted(k=8, per=50, p_in=0.3, p_out=0.005, seed=0):
+    """Undirected graph with k planted communities."""
+    rng = np.random.default_rng(seed)
+    n = k * per
+    blocks = np.repeat(np.arange(k), per)
+    a = rng.random((n, n)) < np.where(blocks[:, None] == blocks[None, :], p_in, p_out)
+    a = np.triu(a, 1)
+    r, c = np.nonzero(a)
+    key = np.unique(np.concatenate([r * n + c, c * n + r]))
+    return n, np.stack([key // n, key % n])
+
+
+def test_partition_is_deterministic_and_balanced():
+    g = synth.bipartite(400, 300, 6000, seed=2)
+    for k in (1, 2, 7, 64):
+        a = cluster.partition_nodes(g.edge_index, g.num_nodes, k)
+        b = cluster.partition_nodes(g.edge_index, g.num_nodes, k)
+        assert np.array_equal(a, b)
+        assert a.min() >= 0 and a.max() < k
+        sizes = cluster.part_sizes(a, k)
+        assert sizes.max() - sizes.min() <= 1 and sizes.sum() == g.num_nodes
+
+
+def test_partition_finds_planted_communities():
+    n, ei = planted()
+    part = cluster.partition_nodes(ei, n, 8)
+    rnd = np.random.default_rng(0).integers(0, 8, n)
+    assert cluster.intra_fraction(ei, part) > 0.6
+    assert cluster.intra_fraction(ei, part) > 3 * cluster.intra_fraction(ei, rnd)
+
+
+def test_partition_beats_random_on_ml25m_shaped():
+    g = synth.ml25m_shaped(seed=0, scale=0.02)
+    part = cluster.partition_nodes(g.edge_index, g.num_nodes, 16)
+    rnd = np.random.default_rng(0).integers(0, 16, g.num_nodes)
+    assert cluster.intra_fraction(g.edge_index, part) > 1.5 * cluster.intra_fraction(g.edge_index, rnd)
+
+
+def test_intra_part_edges_order_and_coverage():
+    g = synth.bipartite(200, 100, 2000, seed=3)
+    ei = g.edge_index
+    part = cluster.partition_nodes(ei, g.num_nodes, 5)
+    lists = cluster.intra_part_edges(ei, part, 5)
+    keep = part[ei[0]] == part[ei[1]]
+    assert sum(x.shape[1] for x in lists) == int(keep.sum())
+    pos = {(int(a), int(b)): i for i, (a, b) in enumerate(ei.T)}
+    for p, x in enumerate(lists):
+        assert np.all(part[x[0]] == p) and np.all(part[x[1]] == p)
+        idx = [pos[(int(a), int(b))] for a, b in x.T]
+        assert idx == sorted(idx)  # input (row, col) order kept, as ClusterData's monotone remap
+
+
+def test_partition_rejects_bad_ids():
+    with pytest.raises(_ffi.LgcnError):
+        cluster.partition_nodes(np.array([[0, 5], [1, 0]]), 3, 2)
+
+
+def test_empty_and_tiny():
+    part = cluster.partition_nodes(np.zeros((2, 0), np.int64), 5, 3)
+    assert sorted(cluster.part_sizes(part, 3).tolist()) == [1, 2, 2]
+    assert cluster.intra_fraction(np.zeros((2, 0), np.int64), part) == 1.0
