@@ -126,7 +126,13 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="graph scale vs ML-25M (1.0 = C2)")
     ap.add_argument("--chunk", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["propagate", "train"], default="propagate",
+                    help="propagate: C2 headline (default); train: C3/C4 Cluster-GCN training steps")
+    ap.add_argument("--parts", type=int, default=1024, help="train: Cluster-GCN parts")
+    ap.add_argument("--parts-per-batch", type=int, default=32, help="train: parts per step")
     args = ap.parse_args()
+    if args.workload == "train":
+        return run_train(args)
 
     import numpy as np
     import torch
@@ -230,6 +236,105 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_train(args):
+    """C3 (1 GPU) / C4 (N GPUs): Cluster-GCN training of LightGCN K=3, d=128 on the ML-25M-shaped
+    graph: 90/5/5 directed split, train graph cut into --parts parts by the host LDG partitioner,
+    --parts-per-batch parts per step (union of intra-part edges), BPR loss, backward through the
+    HIP propagation, clip_grad_norm_(1), Adam(1e-3). N ranks = data parallel: disjoint batches per
+    rank, RCCL all_reduce of the two dense embedding gradients each step (lgcn_amd.distributed).
+    value = K * (batch edges summed over ranks) / wall time."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from data.dataset_handler import Data
+    from lgcn_amd import cluster, synth
+    from lgcn_amd import distributed as D
+    from models.light_gcn import LightGCN
+    from utils.train_test import bpr_loss, compute_embeddings
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    K = args.layers
+    d = args.dim if args.dim != 64 else 128
+    t0 = time.perf_counter()
+    g = synth.ml25m_shaped(seed=0, scale=args.scale)  # one graph, replicated tables (DP)
+    U, I, N = g.num_users, g.num_items, g.num_nodes
+    rng = np.random.default_rng(0)
+    perm = rng.permutation(g.num_edges)
+    n_tr = int(0.9 * g.num_edges)
+    train_ei = np.ascontiguousarray(g.edge_index[:, np.sort(perm[:n_tr])])
+    part = cluster.partition_nodes(train_ei, N, args.parts)
+    f_intra = cluster.intra_fraction(train_ei, part)
+    lists = cluster.intra_part_edges(train_ei, part, args.parts)
+    order = np.random.default_rng(1).permutation(args.parts)
+    q = args.parts_per_batch
+    batches = []
+    for b in range(0, args.parts, q):
+        ei = np.concatenate([lists[p] for p in order[b:b + q]], axis=1)
+        batches.append(Data(edge_index=torch.from_numpy(ei).to(dev), num_nodes=N))
+    log(f"[rank {rank}] train graph E={n_tr} parts={args.parts} f_intra={f_intra:.4f} "
+        f"batches={len(batches)} mean E_batch={np.mean([b.edge_index.shape[1] for b in batches]):.0f} "
+        f"({time.perf_counter() - t0:.1f} s)")
+    torch.manual_seed(0)
+    model = LightGCN(U, I, num_layers=K, dim_h=d).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    params = list(model.parameters())
+    torch.manual_seed(1000 + rank)
+
+    def step(bidx):
+        batch = batches[bidx]
+        opt.zero_grad()
+        loss = bpr_loss(*compute_embeddings(model, batch, dev))
+        loss.backward()
+        D.allreduce_grads(params, world)
+        torch.nn.utils.clip_grad_norm_(params, max_norm=1)
+        opt.step()
+        return batch.edge_index.shape[1]
+
+    share = D.rank_share(len(batches), world, rank, seed=0, epoch=0)
+    for i in range(max(args.warmup, len(share))):  # warm-up builds every batch's plan
+        step(share[i % len(share)])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    edges = 0
+    for i in range(args.steps):
+        edges += step(share[i % len(share)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed, edges], dtype=torch.float64, device=dev)
+        tt = t.clone()
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+        elapsed, edges = float(t[0].item()), float(tt[1].item())
+    result = {
+        "metric": f"training edges propagated/sec (Cluster-GCN, K={K}, d={d})",
+        "value": K * edges / elapsed, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (seeded ML-25M-shaped graph, 90/5/5 directed split)",
+        "config": {"workload": f"C{3 if world == 1 else 4}_cluster_gcn_train", "parts": args.parts,
+                   "parts_per_batch": q, "f_intra": f_intra, "layers": K, "dim": d, "num_users": U,
+                   "num_items": I, "train_edges": n_tr,
+                   "parallelism": f"dp{world}: disjoint part batches per rank, RCCL all_reduce of embedding grads"},
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
