@@ -130,6 +130,7 @@ def main():
                     help="propagate: C2 headline (default); train: C3/C4 Cluster-GCN training steps")
     ap.add_argument("--parts", type=int, default=1024, help="train: Cluster-GCN parts")
     ap.add_argument("--parts-per-batch", type=int, default=32, help="train: parts per step")
+    ap.add_argument("--torch-adam", action="store_true", help="train: torch Adam + clip_grad_norm_ (reference ops)")
     args = ap.parse_args()
     if args.workload == "train":
         return run_train(args)
@@ -164,7 +165,8 @@ def main():
     user_w = (torch.randn(U, d, device=dev, generator=gen) * 0.01).contiguous()
     item_w = (torch.randn(I, d, device=dev, generator=gen) * 0.01).contiguous()
     t0 = time.perf_counter()
-    plan = PropagationPlan(ei, N, args.chunk or DEFAULT_CHUNK)
+    # side_split = U: rows gathering the item table run first, then rows gathering the user table
+    plan = PropagationPlan(ei, N, args.chunk or DEFAULT_CHUNK, side_split=U)
     torch.cuda.synchronize()
     log(f"[rank {rank}] plan: {plan.fwd.n_items} items, {plan.fwd.n_splits} split rows, "
         f"{plan.fwd.n_partials} partials, {plan.nbytes() / 1e6:.0f} MB ({time.perf_counter() - t0:.2f} s)")
@@ -287,7 +289,12 @@ def run_train(args):
         f"({time.perf_counter() - t0:.1f} s)")
     torch.manual_seed(0)
     model = LightGCN(U, I, num_layers=K, dim_h=d).to(dev)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    if args.torch_adam:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    else:
+        from lgcn_amd.optim import FusedAdam
+
+        opt = FusedAdam(model.parameters(), lr=1e-3, max_grad_norm=1)
     params = list(model.parameters())
     torch.manual_seed(1000 + rank)
 
@@ -297,7 +304,8 @@ def run_train(args):
         loss = bpr_loss(*compute_embeddings(model, batch, dev))
         loss.backward()
         D.allreduce_grads(params, world)
-        torch.nn.utils.clip_grad_norm_(params, max_norm=1)
+        if args.torch_adam:
+            torch.nn.utils.clip_grad_norm_(params, max_norm=1)
         opt.step()
         return batch.edge_index.shape[1]
 
@@ -328,6 +336,7 @@ def run_train(args):
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (seeded ML-25M-shaped graph, 90/5/5 directed split)",
         "config": {"workload": f"C{3 if world == 1 else 4}_cluster_gcn_train", "parts": args.parts,
+                   "optimizer": "torch Adam + clip_grad_norm_" if args.torch_adam else "lgcn FusedAdam (clip fused)",
                    "parts_per_batch": q, "f_intra": f_intra, "layers": K, "dim": d, "num_users": U,
                    "num_items": I, "train_edges": n_tr,
                    "parallelism": f"dp{world}: disjoint part batches per rank, RCCL all_reduce of embedding grads"},

@@ -116,13 +116,16 @@ int lgcn_edge_norm(const int64_t* rowptr, const int32_t* col, int64_t N, int64_t
 
 /* ---------------------------------------------------------------------------------------
  * Load-balanced schedule for one plan. Rows longer than `chunk` edges are cut into chunks
- * of `chunk` edges; items are ordered longest-first (stable), so neighbouring 16-lane groups
- * of a wave carry equal work. Capacities: items <= N + E/chunk, splits <= N,
+ * of `chunk` edges. Items of rows [0, side_split) come first, then the others (LightGCN passes
+ * side_split = num_users, so the rows gathering from the item table run together and then the
+ * rows gathering from the user table: each phase has one table's working set in L2); inside a
+ * side items are ordered longest-first (stable), so neighbouring lane groups of a wave carry
+ * equal work. side_split = 0 gives one global longest-first order. Capacities: items <= N + E/chunk, splits <= N,
  * partials <= E/chunk + N. counts[0..2] (device int64) receive n_items, n_splits,
  * n_partials; the caller reads them back once per plan. */
 int lgcn_schedule_workspace_size(int64_t E, int64_t N, int32_t chunk, size_t* bytes);
 int lgcn_schedule_build(const int64_t* rowptr, int64_t N, int64_t E, int32_t chunk,
-                        lgcn_item_t* items, int64_t items_cap,
+                        int64_t side_split, lgcn_item_t* items, int64_t items_cap,
                         lgcn_split_t* splits, int64_t splits_cap,
                         int64_t* counts, void* ws, size_t ws_bytes, lgcn_stream_t stream);
 
@@ -176,6 +179,31 @@ int lgcn_scale(const float* in, float* out, int64_t n, float mul, float div, lgc
  * LightGCN forward (mean over a one-element stack). */
 int lgcn_copy_scale(const float* x_lo, const float* x_hi, int64_t x_split, int64_t N, int32_t d,
                     float* out, float div, float mul, lgcn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Training-step tail (reference utils/train_test.py:95-96: clip_grad_norm_(max_norm=1) then
+ * optim.Adam(lr=1e-3).step() over the two dense embedding tables). Device pointers; the
+ * tensor descriptors themselves are a host array of n (<= 8) entries.
+ *   lgcn_grad_norm: out[0] = ||all grads||_2, out[1] = min(max_norm / (out[0] + 1e-6), 1);
+ *     ws holds lgcn_grad_norm_workspace_floats() floats. Deterministic two-stage reduction.
+ *   lgcn_adam_step: per element g *= clip[1] (clip may be NULL), m += (1-b1)(g-m),
+ *     v = b2 v + (1-b2) g^2, p += step_size * m / (sqrt(v)/bc2_sqrt + eps), with
+ *     step_size = -lr/(1-b1^t) and bc2_sqrt = sqrt(1-b2^t) computed by the caller in double
+ *     (as torch does); write_grad != 0 also stores the clipped g back. */
+typedef struct {
+    float* param;
+    float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t numel;
+} lgcn_adam_tensor_t;
+
+int lgcn_grad_norm_workspace_floats(void);
+int lgcn_grad_norm(const lgcn_adam_tensor_t* tensors, int32_t n, float max_norm, float* ws, float* out,
+                   lgcn_stream_t stream);
+int lgcn_adam_step(const lgcn_adam_tensor_t* tensors, int32_t n, float one_minus_beta1, float beta2,
+                   float one_minus_beta2, float eps, float step_size, float bc2_sqrt, const float* clip,
+                   int32_t write_grad, lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Host-side (no GPU): balanced k-way node partition for Cluster-GCN batching, the METIS

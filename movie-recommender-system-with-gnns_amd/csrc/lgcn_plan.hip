@@ -109,7 +109,7 @@ __global__ void k_fill_u32(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
 }
 
-__global__ void k_sched_fill(const int64_t* __restrict__ rowptr, int64_t N, int32_t chunk,
+__global__ void k_sched_fill(const int64_t* __restrict__ rowptr, int64_t N, int32_t chunk, int64_t side_split,
                              const int64_t* __restrict__ n_items, const int64_t* __restrict__ item_off,
                              const int32_t* __restrict__ n_part, const int32_t* __restrict__ part_off,
                              const int32_t* __restrict__ n_split, const int32_t* __restrict__ split_off,
@@ -129,7 +129,9 @@ __global__ void k_sched_fill(const int64_t* __restrict__ rowptr, int64_t N, int3
             it.len = static_cast<int32_t>(rem < chunk ? rem : chunk);
             it.dst = (nch > 1) ? -(part_off[i] + static_cast<int32_t>(c)) - 1 : static_cast<int32_t>(i);
             raw[off + c] = it;
-            keys[off + c] = static_cast<uint32_t>(chunk - it.len);  // longest first
+            // rows [0, side_split) first, then the rest; longest first inside each side
+            const uint32_t side = (i >= side_split) ? 1u : 0u;
+            keys[off + c] = (side << 31) | static_cast<uint32_t>(chunk - it.len);
             idx[off + c] = static_cast<int32_t>(off + c);
         }
         if (nch > 1) {
@@ -175,7 +177,7 @@ size_t sched_cub_bytes(int64_t E, int64_t N, int32_t chunk) {
                                      static_cast<int>(N));
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                        (const int32_t*)nullptr, (int32_t*)nullptr,
-                                       static_cast<int>(cap), 0, key_bits(int64_t(chunk) + 2));
+                                       static_cast<int>(cap), 0, 32);
     size_t m = a > b ? a : b;
     return m > c ? m : c;
 }
@@ -275,11 +277,11 @@ int lgcn_schedule_workspace_size(int64_t E, int64_t N, int32_t chunk, size_t* by
     return LGCN_OK;
 }
 
-int lgcn_schedule_build(const int64_t* rowptr, int64_t N, int64_t E, int32_t chunk,
+int lgcn_schedule_build(const int64_t* rowptr, int64_t N, int64_t E, int32_t chunk, int64_t side_split,
                         lgcn_item_t* items, int64_t items_cap, lgcn_split_t* splits,
                         int64_t splits_cap, int64_t* counts, void* ws, size_t ws_bytes,
                         lgcn_stream_t stream) {
-    if (!rowptr || !counts || N < 0 || E < 0 || chunk < 1)
+    if (!rowptr || !counts || N < 0 || E < 0 || chunk < 1 || chunk >= (1 << 30) || side_split < 0)
         return fail(LGCN_E_ARG, "lgcn_schedule_build: bad args");
     if (N > INT32_MAX || E > INT32_MAX) return fail(LGCN_E_UNSUPPORTED, "schedule: sizes exceed int32");
     hipStream_t s = as_stream(stream);
@@ -314,18 +316,17 @@ int lgcn_schedule_build(const int64_t* rowptr, int64_t N, int64_t E, int32_t chu
     t = cub_bytes;
     if (int rc = check_hip(hipcub::DeviceScan::ExclusiveSum(cub_tmp, t, n_split, split_off, static_cast<int>(N), s), "scan splits")) return rc;
     // padding slots [n_items, cap) sort last (key = chunk + 1) and are never read
-    const uint32_t pad_key = static_cast<uint32_t>(chunk) + 1u;
+    const uint32_t pad_key = 0xFFFFFFFFu;  // sorts after both sides
     k_fill_u32<<<grid_for(cap, kBlock, 8192), kBlock, 0, s>>>(k_in, cap, pad_key);
     if (int rc = check_launch("k_fill_u32")) return rc;
     k_fill_u32<<<grid_for(cap, kBlock, 8192), kBlock, 0, s>>>(reinterpret_cast<uint32_t*>(i_in), cap, 0u);
     if (int rc = check_launch("k_fill_u32")) return rc;
-    k_sched_fill<<<g, kBlock, 0, s>>>(rowptr, N, chunk, n_items, item_off, n_part, part_off, n_split,
+    k_sched_fill<<<g, kBlock, 0, s>>>(rowptr, N, chunk, side_split, n_items, item_off, n_part, part_off, n_split,
                                       split_off, raw, k_in, i_in, splits, counts);
     if (int rc = check_launch("k_sched_fill")) return rc;
     t = cub_bytes;
     if (int rc = check_hip(hipcub::DeviceRadixSort::SortPairs(cub_tmp, t, k_in, k_out, i_in, i_out,
-                                                              static_cast<int>(cap), 0,
-                                                              key_bits(int64_t(chunk) + 2), s),
+                                                              static_cast<int>(cap), 0, 32, s),
                            "SortPairs(schedule)"))
         return rc;
     // gather all cap slots; the tail beyond n_items is padding the kernels never index

@@ -39,7 +39,7 @@ _SIGS = {
     "lgcn_inv_sqrt_degree": ([_vp, _i64, _vp, _vp], ctypes.c_int),
     "lgcn_edge_norm": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_schedule_workspace_size": ([_i64, _i64, _i32, ctypes.POINTER(_sz)], ctypes.c_int),
-    "lgcn_schedule_build": ([_vp, _i64, _i64, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _sz, _vp], ctypes.c_int),
+    "lgcn_schedule_build": ([_vp, _i64, _i64, _i32, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _sz, _vp], ctypes.c_int),
     "lgcn_spmm": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
                    _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp],
                   ctypes.c_int),
@@ -51,11 +51,19 @@ _SIGS = {
                           ctypes.c_int),
     "lgcn_scale": ([_vp, _vp, _i64, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_copy_scale": ([_vp, _vp, _i64, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),
+    "lgcn_grad_norm_workspace_floats": ([], ctypes.c_int),
+    "lgcn_grad_norm": ([_vp, _i32, _f32, _vp, _vp, _vp], ctypes.c_int),
+    "lgcn_adam_step": ([_vp, _i32, _f32, _f32, _f32, _f32, _f32, _f32, _vp, _i32, _vp], ctypes.c_int),
     "lgcn_partition_edges": ([_vp, _vp, _i64, _i64, _i32, _i32, _f32, _vp], ctypes.c_int),
     "lgcn_partition_last_error": ([], ctypes.c_char_p),
 }
 
 EXPORTED = tuple(_SIGS)
+
+
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("numel", ctypes.c_int64)]
 
 
 class LgcnError(RuntimeError):

@@ -64,7 +64,8 @@ def train_epoch(model, optimizer, batches, device, seed: int = 0, epoch: int = 0
         loss = loss_fn(*embed_fn(model, batch, device))
         loss.backward()
         allreduce_grads(params, world)
-        torch.nn.utils.clip_grad_norm_(params, max_norm=max_norm)
+        if getattr(optimizer, "fused_clip_norm", None) is None:
+            torch.nn.utils.clip_grad_norm_(params, max_norm=max_norm)
         optimizer.step()
         w = batch.edge_index.shape[1]
         acc[0] += loss.detach().double() * w

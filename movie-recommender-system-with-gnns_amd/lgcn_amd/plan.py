@@ -44,7 +44,7 @@ class CsrDirection:
         return torch.stack([it[:, 0], lens_dst[:, 0].long(), lens_dst[:, 1].long()], dim=1)
 
 
-def _build_direction(key: torch.Tensor, other: torch.Tensor, N: int, chunk: int,
+def _build_direction(key: torch.Tensor, other: torch.Tensor, N: int, chunk: int, side_split: int,
                      dis: torch.Tensor | None, stream: int) -> tuple[CsrDirection, torch.Tensor, int]:
     lib = _ffi.load()
     dev = key.device
@@ -72,7 +72,7 @@ def _build_direction(key: torch.Tensor, other: torch.Tensor, N: int, chunk: int,
     items = torch.empty((cap, 2), dtype=torch.int64, device=dev)
     splits = torch.empty((max(N, 1), 4), dtype=torch.int32, device=dev)
     counts = torch.zeros(3, dtype=torch.int64, device=dev)
-    _ffi.check(lib.lgcn_schedule_build(rowptr.data_ptr(), N, E, chunk, items.data_ptr(), cap, splits.data_ptr(),
+    _ffi.check(lib.lgcn_schedule_build(rowptr.data_ptr(), N, E, chunk, side_split, items.data_ptr(), cap, splits.data_ptr(),
                                        splits.shape[0], counts.data_ptr(), ws2.data_ptr(), ws2.numel(), stream),
                "lgcn_schedule_build")
     # one host read-back per plan: ids check + schedule sizes (the launches need them)
@@ -85,7 +85,7 @@ def _build_direction(key: torch.Tensor, other: torch.Tensor, N: int, chunk: int,
 class PropagationPlan:
     """Forward (+ lazily transposed) plan for one edge set over N = num_users + num_items nodes."""
 
-    def __init__(self, edge_index: torch.Tensor, num_nodes: int, chunk: int = DEFAULT_CHUNK):
+    def __init__(self, edge_index: torch.Tensor, num_nodes: int, chunk: int = DEFAULT_CHUNK, side_split: int = 0):
         _ffi.require_device(edge_index, "PropagationPlan")
         if edge_index.dim() != 2 or edge_index.shape[0] != 2:
             raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
@@ -94,12 +94,14 @@ class PropagationPlan:
         self.num_nodes = int(num_nodes)
         self.num_edges = int(edge_index.shape[1])
         self.chunk = int(chunk)
+        self.side_split = int(side_split)
         self.device = edge_index.device
         self._src = edge_index[0].contiguous()
         self._dst = edge_index[1].contiguous()
         stream = _ffi.stream_of(self.device)
         # forward: rows = targets (PyG flow source_to_target aggregates at edge_index[1])
-        self.fwd, self.dis, bad = _build_direction(self._dst, self._src, self.num_nodes, self.chunk, None, stream)
+        self.fwd, self.dis, bad = _build_direction(self._dst, self._src, self.num_nodes, self.chunk,
+                                                 self.side_split, None, stream)
         if bad:
             raise IndexError(f"edge_index holds {bad} edge(s) with a node id outside [0, {self.num_nodes})")
         self._bwd: CsrDirection | None = None
@@ -110,7 +112,8 @@ class PropagationPlan:
         forward in-degree normalisation, so val_T[q] == val[edge] exactly."""
         if self._bwd is None:
             stream = _ffi.stream_of(self.device)
-            self._bwd, _, _ = _build_direction(self._src, self._dst, self.num_nodes, self.chunk, self.dis, stream)
+            self._bwd, _, _ = _build_direction(self._src, self._dst, self.num_nodes, self.chunk,
+                                              self.side_split, self.dis, stream)
         return self._bwd
 
     def nbytes(self) -> int:
@@ -132,9 +135,9 @@ class PlanCache:
         self.chunk = chunk
         self._entries: dict[tuple, tuple[weakref.ref, PropagationPlan]] = {}
 
-    def get(self, edge_index: torch.Tensor, num_nodes: int) -> PropagationPlan:
+    def get(self, edge_index: torch.Tensor, num_nodes: int, side_split: int = 0) -> PropagationPlan:
         key = (id(edge_index), edge_index.data_ptr(), tuple(edge_index.shape), tuple(edge_index.stride()),
-               edge_index._version, int(num_nodes), str(edge_index.device))
+               edge_index._version, int(num_nodes), int(side_split), str(edge_index.device))
         hit = self._entries.get(key)
         if hit is not None:
             ref, plan = hit
@@ -144,7 +147,7 @@ class PlanCache:
                 self._entries[key] = hit
                 return plan
             self._entries.pop(key)
-        plan = PropagationPlan(edge_index, num_nodes, self.chunk)
+        plan = PropagationPlan(edge_index, num_nodes, self.chunk, side_split)
         self._entries[key] = (weakref.ref(edge_index), plan)
         self._evict()
         return plan

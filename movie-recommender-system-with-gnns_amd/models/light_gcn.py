@@ -45,7 +45,7 @@ class LightGCN(nn.Module):
 
     def plan_for(self, edge_index):
         """The cached propagation plan of an edge set (built on first use)."""
-        return self._plans.get(edge_index, self.num_users + self.num_items)
+        return self._plans.get(edge_index, self.num_users + self.num_items, side_split=self.num_users)
 
     def forward(self, edge_index):
         plan = self.plan_for(edge_index)

@@ -76,8 +76,9 @@ def train(model: torch.nn.Module, optimizer: torch.optim.Optimizer, train_loader
         optimizer.zero_grad()
         loss = bpr_loss(*compute_embeddings(model, batch, device))
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1)
-        optimizer.step()
+        if getattr(optimizer, "fused_clip_norm", None) is None:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1)
+        optimizer.step()  # lgcn_amd.optim.FusedAdam(max_grad_norm=1) clips inside its step
         w = batch.edge_index.shape[1]
         total_w += w
         contrib = loss.detach().double() * w
@@ -120,10 +121,16 @@ def evaluate(model: torch.nn.Module, test_data, device, top_k: int = 100):
 
 
 def train_model(model: torch.nn.Module, train_loader, val_data, test_data, device, epochs: int = 1,
-                lr: float = 0.001, checkpoint: str = "best_model.pth"):
-    """Epoch loop with validation and best-recall checkpointing (reference :214-256)."""
+                lr: float = 0.001, checkpoint: str = "best_model.pth", fused_optimizer: bool = False):
+    """Epoch loop with validation and best-recall checkpointing (reference :214-256).
+    fused_optimizer=True swaps torch Adam + clip_grad_norm_ for the two-launch HIP FusedAdam."""
     hist_train_loss, hist_val_loss, hist_val_recall = [], [], []
-    optimizer = optim.Adam(model.parameters(), lr=lr)
+    if fused_optimizer:
+        from lgcn_amd.optim import FusedAdam
+
+        optimizer = FusedAdam(model.parameters(), lr=lr, max_grad_norm=1)
+    else:
+        optimizer = optim.Adam(model.parameters(), lr=lr)
     best_recall = 0
     for epoch in tqdm(range(epochs)):
         loss = train(model, optimizer, train_loader, device)

@@ -104,3 +104,31 @@ def test_cluster_training_converges_on_gpu(gpu):
     _, tr, vl, vr = TT.train_model(model, loader, val, test, gpu, epochs=4, lr=1e-2, checkpoint=None)
     assert all(np.isfinite(tr)) and tr[-1] < tr[0]
     assert all(0.0 <= r <= 1.0 for r in vr)
+
+
+def test_fused_adam_matches_torch(gpu):
+    """FusedAdam(max_grad_norm=1) == clip_grad_norm_(1) + torch Adam, to fp32 rounding."""
+    from lgcn_amd.optim import FusedAdam
+
+    torch.manual_seed(0)
+    shapes = [(1000, 64), (333, 64), (7, 3)]
+    a = [torch.randn(s, device=gpu) * 0.01 for s in shapes]
+    b = [t.clone() for t in a]
+    pa = [torch.nn.Parameter(t) for t in a]
+    pb = [torch.nn.Parameter(t) for t in b]
+    oa = torch.optim.Adam(pa, lr=1e-3)
+    ob = FusedAdam(pb, lr=1e-3, max_grad_norm=1)
+    for step in range(6):
+        scale = 10.0 if step % 2 == 0 else 0.01  # clipping active / inactive
+        gs = [torch.randn(s, device=gpu) * scale for s in shapes]
+        for p, g in zip(pa, gs):
+            p.grad = g.clone()
+        for p, g in zip(pb, gs):
+            p.grad = g.clone()
+        norm = torch.nn.utils.clip_grad_norm_(pa, max_norm=1)
+        oa.step()
+        ob.step()
+        assert abs(ob.last_norm[0].item() - norm.item()) <= 1e-5 * norm.item()
+        for x, y in zip(pa, pb):
+            assert torch.allclose(x.grad, y.grad, rtol=1e-5, atol=1e-9)
+            assert (x - y).abs().max().item() <= 1e-6 * max(1.0, x.abs().max().item()) + 1e-8
