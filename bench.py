@@ -86,6 +86,15 @@ def load_traffic(workload: str):
         return None
 
 
+def init_dist(backend, dev):
+    import torch.distributed as dist
+
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(backend)
+
+
 def cpu_baseline(graph, K, d, seconds_budget=20.0):
     """Reference CPU path (torch primitives of PyG 2.4.0 LGConv) on a bounded edge sample."""
     import numpy as np
@@ -130,7 +139,11 @@ def main():
                     help="propagate: C2 headline (default); train: C3/C4 Cluster-GCN training steps")
     ap.add_argument("--parts", type=int, default=1024, help="train: Cluster-GCN parts")
     ap.add_argument("--parts-per-batch", type=int, default=32, help="train: parts per step")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for runs; gloo to rehearse N ranks on one GPU")
     ap.add_argument("--torch-adam", action="store_true", help="train: torch Adam + clip_grad_norm_ (reference ops)")
+    ap.add_argument("--autograd", action="store_true",
+                    help="train: reference-style step (compute_embeddings + bpr_loss + autograd) instead of "
+                         "the fused no-autograd step")
     args = ap.parse_args()
     if args.workload == "train":
         return run_train(args)
@@ -148,11 +161,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     distributed = world > 1
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        init_dist(args.dist_backend, dev)
 
     K, d = args.layers, args.dim
     t0 = time.perf_counter()
@@ -262,10 +275,10 @@ def run_train(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        init_dist(args.dist_backend, dev)
     K = args.layers
     d = args.dim if args.dim != 64 else 128
     t0 = time.perf_counter()
@@ -298,8 +311,17 @@ def run_train(args):
     params = list(model.parameters())
     torch.manual_seed(1000 + rank)
 
+    fused = None
+    if not args.autograd:
+        from lgcn_amd.train_step import FusedTrainStep
+
+        fused = FusedTrainStep(model, opt, world=world)
+
     def step(bidx):
         batch = batches[bidx]
+        if fused is not None:
+            fused.step(batch)
+            return batch.edge_index.shape[1]
         opt.zero_grad()
         loss = bpr_loss(*compute_embeddings(model, batch, dev))
         loss.backward()
@@ -310,7 +332,7 @@ def run_train(args):
         return batch.edge_index.shape[1]
 
     share = D.rank_share(len(batches), world, rank, seed=0, epoch=0)
-    for i in range(max(args.warmup, len(share))):  # warm-up builds every batch's plan
+    for i in range(max(args.warmup, 2 * len(share))):  # warm-up builds every batch's plan
         step(share[i % len(share)])
     if world > 1:
         dist.barrier()
@@ -337,6 +359,7 @@ def run_train(args):
         "data": "synthetic (seeded ML-25M-shaped graph, 90/5/5 directed split)",
         "config": {"workload": f"C{3 if world == 1 else 4}_cluster_gcn_train", "parts": args.parts,
                    "optimizer": "torch Adam + clip_grad_norm_" if args.torch_adam else "lgcn FusedAdam (clip fused)",
+                   "step": "autograd (reference ops)" if args.autograd else "fused (lgcn_bpr_fused + sorted scatter)",
                    "parts_per_batch": q, "f_intra": f_intra, "layers": K, "dim": d, "num_users": U,
                    "num_items": I, "train_edges": n_tr,
                    "parallelism": f"dp{world}: disjoint part batches per rank, RCCL all_reduce of embedding grads"},

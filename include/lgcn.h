@@ -181,6 +181,25 @@ int lgcn_copy_scale(const float* x_lo, const float* x_hi, int64_t x_split, int64
                     float* out, float div, float mul, lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Fused cosine-BPR loss + gradient (reference utils/train_test.py:18-64 bpr_loss over the six
+ * gathers of compute_embeddings :105-134). Triplet b = (u[b], p[b], n[b]) (user id, item ids).
+ * F: propagated table (split; user u at row u, item i at row U+i), W: layer-0 table (same).
+ *   lgcn_bpr_fused writes, per triplet, dF rows cf[b], cf[B+b], cf[2B+b] (d loss / d F rows of
+ *   u, p, n), reg-gradient rows cw[...] (d loss / d W rows) and terms[b] = softplus term,
+ *   terms[B+b] = sum of squares of the three W rows. d in {16,32,64,128,256,512}.
+ *   lgcn_bpr_loss: loss[0] = -(mean softplus)/10 + coeff * sum(squares)/(B*d).
+ *   lgcn_segment_rows: out[r] (+)= sum of C[perm[e]] for e in [rowptr[r], rowptr[r+1]) in order —
+ *   the deterministic scatter of those rows, with rowptr/perm from lgcn_csr_build over the 3B keys
+ *   (u, U+p, U+n). add == 0 writes every row (0 where empty); add != 0 only adds. */
+int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split,
+                   const float* w_lo, const float* w_hi, int64_t w_split, int64_t U,
+                   const int64_t* u, const int64_t* p, const int64_t* n, int64_t B, int32_t d,
+                   float coeff, float* cf, float* cw, float* terms, lgcn_stream_t stream);
+int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* loss, lgcn_stream_t stream);
+int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C, int64_t N, int32_t d,
+                      float* out_lo, float* out_hi, int64_t split, int32_t add, lgcn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * Training-step tail (reference utils/train_test.py:95-96: clip_grad_norm_(max_norm=1) then
  * optim.Adam(lr=1e-3).step() over the two dense embedding tables). Device pointers; the
  * tensor descriptors themselves are a host array of n (<= 8) entries.

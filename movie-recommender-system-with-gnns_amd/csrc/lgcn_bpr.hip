@@ -1,0 +1,276 @@
+// Fused cosine-BPR loss and its gradient for the Cluster-GCN training step (gfx950).
+//
+// Reference utils/train_test.py:105-134 (compute_embeddings: six row gathers) and :18-64
+// (bpr_loss: L2 reg on layer-0 rows, row-normalised cosines, softplus(10 * margin)):
+//   loss = -mean_b softplus(10 (cos(u_b, p_b) - cos(u_b, n_b))) / 10
+//          + coeff * mean_{b,c} (eu_bc^2 + ep_bc^2 + en_bc^2)
+// PyTorch runs this as ~25 elementwise/reduction launches forward, ~30 backward, and scatters
+// the row gradients with a sort-based index_put_. Here:
+//   k_bpr_fused   one lane group per triplet: loads the 6 rows once (propagated F rows for the
+//                 cosines, layer-0 W rows for the reg term), reduces the 6 dot products inside
+//                 the group, and writes the per-triplet gradient rows (dF for u, p, n and the
+//                 reg gradient for W) plus the two loss terms — no atomics;
+//   k_bpr_loss    deterministic single-block sum of the loss terms;
+//   k_segment_rows  adds the gradient rows into their destination rows in a fixed (stable
+//                 sorted) order using the CSR lgcn_csr_build makes of the 3B row keys.
+// The gradient is the analytic derivative of the same expression (not bitwise torch autograd).
+
+#include "lgcn_common.h"
+
+using namespace lgcn;
+
+namespace {
+
+template <class T>
+__device__ __forceinline__ T* srow(T* lo, T* hi, int64_t split, int64_t r, int64_t stride) {
+    return (r < split) ? lo + r * stride : hi + (r - split) * stride;
+}
+
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+    for (int off = LPR / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, LPR);
+    return v;
+}
+
+__device__ __forceinline__ float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+
+struct BprArgs {
+    const float* f_lo;
+    const float* f_hi;
+    int64_t f_split;
+    const float* w_lo;
+    const float* w_hi;
+    int64_t w_split;
+    int64_t U;
+    const int64_t* u;
+    const int64_t* p;
+    const int64_t* n;
+    int64_t B;
+    int32_t d;
+    float coeff;
+    float* cf;     // [3B, d] dF rows (u | p | n)
+    float* cw;     // [3B, d] reg-gradient rows for W (u | p | n)
+    float* terms;  // [2B]: softplus terms | reg row sums
+};
+
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
+    constexpr int GPB = kBlock / LPR;
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    const int64_t b = int64_t(blockIdx.x) * GPB + g;
+    if (b >= a.B) return;
+    const int64_t d = a.d;
+    const int64_t ru = a.u[b];
+    const int64_t rp = a.U + a.p[b];
+    const int64_t rn = a.U + a.n[b];
+    const float4* fu = reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, ru, d)) + l;
+    const float4* fp = reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, rp, d)) + l;
+    const float4* fn = reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, rn, d)) + l;
+    const float4* wu = reinterpret_cast<const float4*>(srow(a.w_lo, a.w_hi, a.w_split, ru, d)) + l;
+    const float4* wp = reinterpret_cast<const float4*>(srow(a.w_lo, a.w_hi, a.w_split, rp, d)) + l;
+    const float4* wn = reinterpret_cast<const float4*>(srow(a.w_lo, a.w_hi, a.w_split, rn, d)) + l;
+    float4 U_[NV], P_[NV], N_[NV], WU[NV], WP[NV], WN[NV];
+    float suu = 0.f, spp = 0.f, snn = 0.f, sup = 0.f, sun = 0.f, sreg = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        U_[k] = fu[k * LPR];
+        P_[k] = fp[k * LPR];
+        N_[k] = fn[k * LPR];
+        WU[k] = wu[k * LPR];
+        WP[k] = wp[k * LPR];
+        WN[k] = wn[k * LPR];
+        suu += dot4(U_[k], U_[k]);
+        spp += dot4(P_[k], P_[k]);
+        snn += dot4(N_[k], N_[k]);
+        sup += dot4(U_[k], P_[k]);
+        sun += dot4(U_[k], N_[k]);
+        sreg += dot4(WU[k], WU[k]) + dot4(WP[k], WP[k]) + dot4(WN[k], WN[k]);
+    }
+    suu = group_sum<LPR>(suu);
+    spp = group_sum<LPR>(spp);
+    snn = group_sum<LPR>(snn);
+    sup = group_sum<LPR>(sup);
+    sun = group_sum<LPR>(sun);
+    sreg = group_sum<LPR>(sreg);
+    const float nu = sqrtf(suu), np = sqrtf(spp), nn = sqrtf(snn);
+    const float cp = sup / (nu * np);
+    const float cn = sun / (nu * nn);
+    const float z = 10.0f * (cp - cn);
+    // F.softplus(beta=1, threshold=20) and its derivative
+    const float sp = (z > 20.0f) ? z : log1pf(expf(z));
+    const float sg = (z > 20.0f) ? 1.0f : 1.0f / (1.0f + expf(-z));
+    const float inv_b = 1.0f / static_cast<float>(a.B);
+    const float dcp = -sg * inv_b;  // d loss / d cos(u,p)
+    const float dcn = sg * inv_b;   // d loss / d cos(u,n)
+    const float kreg = a.coeff * 2.0f / (static_cast<float>(a.B) * static_cast<float>(a.d));
+    const float inu = 1.0f / nu, inp = 1.0f / np, inn = 1.0f / nn;
+    float4* cfu = reinterpret_cast<float4*>(a.cf + b * d) + l;
+    float4* cfp = reinterpret_cast<float4*>(a.cf + (a.B + b) * d) + l;
+    float4* cfn = reinterpret_cast<float4*>(a.cf + (2 * a.B + b) * d) + l;
+    float4* cwu = reinterpret_cast<float4*>(a.cw + b * d) + l;
+    float4* cwp = reinterpret_cast<float4*>(a.cw + (a.B + b) * d) + l;
+    float4* cwn = reinterpret_cast<float4*>(a.cw + (2 * a.B + b) * d) + l;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        float4 du, dp, dn;
+#define LGCN_BPR_LANE(c)                                                                 \
+    {                                                                                    \
+        const float av = U_[k].c * inu, bv = P_[k].c * inp, cv = N_[k].c * inn;           \
+        du.c = (dcp * (bv - cp * av) + dcn * (cv - cn * av)) * inu;                      \
+        dp.c = dcp * (av - cp * bv) * inp;                                               \
+        dn.c = dcn * (av - cn * cv) * inn;                                               \
+    }
+        LGCN_BPR_LANE(x) LGCN_BPR_LANE(y) LGCN_BPR_LANE(z) LGCN_BPR_LANE(w)
+#undef LGCN_BPR_LANE
+        cfu[k * LPR] = du;
+        cfp[k * LPR] = dp;
+        cfn[k * LPR] = dn;
+        cwu[k * LPR] = make_float4(kreg * WU[k].x, kreg * WU[k].y, kreg * WU[k].z, kreg * WU[k].w);
+        cwp[k * LPR] = make_float4(kreg * WP[k].x, kreg * WP[k].y, kreg * WP[k].z, kreg * WP[k].w);
+        cwn[k * LPR] = make_float4(kreg * WN[k].x, kreg * WN[k].y, kreg * WN[k].z, kreg * WN[k].w);
+    }
+    if (l == 0) {
+        a.terms[b] = sp;
+        a.terms[a.B + b] = sreg;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_bpr_loss(const float* __restrict__ terms, int64_t B, int32_t d,
+                                                     float coeff, float* __restrict__ loss) {
+    __shared__ float r0[kBlock / 64], r1[kBlock / 64];
+    float s0 = 0.f, s1 = 0.f;
+    for (int64_t i = threadIdx.x; i < B; i += blockDim.x) {
+        s0 += terms[i];
+        s1 += terms[B + i];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        s0 += __shfl_down(s0, off, 64);
+        s1 += __shfl_down(s1, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        r0[threadIdx.x >> 6] = s0;
+        r1[threadIdx.x >> 6] = s1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float a = 0.f, c = 0.f;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            a += r0[w];
+            c += r1[w];
+        }
+        const float bf = static_cast<float>(B);
+        // -(mean softplus) / 10 + coeff * mean(squares); B == 0 gives NaN, as torch's empty mean
+        loss[0] = -((a / bf) / 10.0f) + coeff * (c / (bf * static_cast<float>(d)));
+    }
+}
+
+// out[r] = sum of C rows perm[rowptr[r] .. rowptr[r+1]) in order (add == 0: every row written,
+// 0 for empty rows); add != 0: out[r] += that sum, rows without contributions untouched.
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_segment_rows(const int64_t* __restrict__ rowptr,
+                                                         const int32_t* __restrict__ perm,
+                                                         const float* __restrict__ C, int64_t N, int32_t d,
+                                                         float* out_lo, float* out_hi, int64_t split, int add) {
+    constexpr int GPB = kBlock / LPR;
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    const int64_t r = int64_t(blockIdx.x) * GPB + g;
+    if (r >= N) return;
+    const int64_t beg = rowptr[r], end = rowptr[r + 1];
+    if (add && beg == end) return;
+    float4 acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t e = beg; e < end; ++e) {
+        const float4* c = reinterpret_cast<const float4*>(C + int64_t(perm[e]) * d) + l;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const float4 v = c[k * LPR];
+            acc[k] = make_float4(acc[k].x + v.x, acc[k].y + v.y, acc[k].z + v.z, acc[k].w + v.w);
+        }
+    }
+    float4* o = reinterpret_cast<float4*>(srow(out_lo, out_hi, split, r, int64_t(d))) + l;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        if (add) {
+            const float4 v = o[k * LPR];
+            acc[k] = make_float4(v.x + acc[k].x, v.y + acc[k].y, v.z + acc[k].z, v.w + acc[k].w);
+        }
+        o[k * LPR] = acc[k];
+    }
+}
+
+template <int LPR, int NV>
+int launch_bpr(const BprArgs& a, hipStream_t s) {
+    constexpr int GPB = kBlock / LPR;
+    const int64_t blocks = (a.B + GPB - 1) / GPB;
+    if (blocks > 0) k_bpr_fused<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+    return check_launch("k_bpr_fused");
+}
+
+template <int LPR, int NV>
+int launch_seg(const int64_t* rowptr, const int32_t* perm, const float* C, int64_t N, int32_t d, float* lo, float* hi,
+               int64_t split, int add, hipStream_t s) {
+    constexpr int GPB = kBlock / LPR;
+    const int64_t blocks = (N + GPB - 1) / GPB;
+    k_segment_rows<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(rowptr, perm, C, N, d, lo, hi,
+                                                                                  split, add);
+    return check_launch("k_segment_rows");
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split, const float* w_lo, const float* w_hi,
+                   int64_t w_split, int64_t U, const int64_t* u, const int64_t* p, const int64_t* n, int64_t B,
+                   int32_t d, float coeff, float* cf, float* cw, float* terms, lgcn_stream_t stream) {
+    if (B < 0 || d <= 0 || U < 0) return fail(LGCN_E_ARG, "lgcn_bpr_fused: bad sizes");
+    if (B == 0) return LGCN_OK;
+    if (!f_lo || !w_lo || !u || !p || !n || !cf || !cw || !terms)
+        return fail(LGCN_E_ARG, "lgcn_bpr_fused: null pointer");
+    if (d % 4 != 0 || !al16(f_lo) || !al16(w_lo) || (f_hi && !al16(f_hi)) || (w_hi && !al16(w_hi)) || !al16(cf) ||
+        !al16(cw))
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_bpr_fused: needs d %% 4 == 0 and 16-byte aligned rows (d=%d)", d);
+    BprArgs a{f_lo, f_hi, f_split, w_lo, w_hi, w_split, U, u, p, n, B, d, coeff, cf, cw, terms};
+    hipStream_t s = as_stream(stream);
+    switch (d) {
+        case 16: return launch_bpr<4, 1>(a, s);
+        case 32: return launch_bpr<8, 1>(a, s);
+        case 64: return launch_bpr<16, 1>(a, s);
+        case 128: return launch_bpr<32, 1>(a, s);
+        case 256: return launch_bpr<64, 1>(a, s);
+        case 512: return launch_bpr<64, 2>(a, s);
+        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_bpr_fused: d=%d (supported 16..512, powers of two)", d);
+    }
+}
+
+int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* loss, lgcn_stream_t stream) {
+    if (B < 0 || !loss || (B > 0 && !terms)) return fail(LGCN_E_ARG, "lgcn_bpr_loss: bad args");
+    k_bpr_loss<<<1, kBlock, 0, as_stream(stream)>>>(terms, B, d, coeff, loss);
+    return check_launch("k_bpr_loss");
+}
+
+int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C, int64_t N, int32_t d,
+                      float* out_lo, float* out_hi, int64_t split, int32_t add, lgcn_stream_t stream) {
+    if (N < 0 || d <= 0 || !rowptr || !out_lo || (split < N && !out_hi)) return fail(LGCN_E_ARG, "lgcn_segment_rows: bad args");
+    if (N == 0) return LGCN_OK;
+    if (d % 4 != 0 || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C && !al16(C)))
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_segment_rows: needs d %% 4 == 0 and aligned rows");
+    hipStream_t s = as_stream(stream);
+    switch (d) {
+        case 16: return launch_seg<4, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
+        case 32: return launch_seg<8, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
+        case 64: return launch_seg<16, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
+        case 128: return launch_seg<32, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
+        case 256: return launch_seg<64, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
+        case 512: return launch_seg<64, 2>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
+        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_segment_rows: d=%d (supported 16..512, powers of two)", d);
+    }
+}
+
+}  // extern "C"
