@@ -8,9 +8,12 @@
 // 16 lanes; one group owns one schedule item (a whole row, or a <= chunk-edge piece of a long
 // row); each lane owns one float4 column slice, so one wave-instruction gathers 4 neighbour
 // rows (1 KiB) with global_load_dwordx4. Items are ordered longest-first, so the 4 groups of a
-// wave carry (nearly) equal work. Neighbour ids/weights are loaded once per 16-edge batch,
-// coalesced, and broadcast inside the group by cross-lane permute; UNROLL gathers are issued
-// before the first add, so every wave keeps several KiB in flight.
+// wave carry (nearly) equal work. Neighbour ids/weights are loaded once per 16-edge batch
+// (prefetched one batch ahead), coalesced, and broadcast inside the group by cross-lane permute;
+// UNROLL gathers are issued before the first add, so every wave keeps several KiB in flight.
+// Measured alternatives that did not pay on C2 (tools/variants.py, profiles/r01c_final/):
+// XCD-aware column split (each XCD one 128-B or 64-B slice of every row: +5% / +100% time),
+// 16-deep unroll, non-temporal col/val loads (within 1%).
 //
 // Numerics: per row, v = (((0 + w0*x0) + w1*x1) + ...) in CSR order, mul then add (no FMA:
 // this file is built with -ffp-contract=off), i.e. the order and rounding of PyG's CPU
@@ -97,29 +100,37 @@ __device__ __forceinline__ void finish_row_vec(const SpmmArgs& a, int64_t r, int
     }
 }
 
+// The item pass. Group g of the block owns item blockIdx*GPB + g. Per 16-edge (LPR-edge) batch
+// the lanes load (col, val) coalesced — the NEXT batch's pair is loaded before the current
+// batch's gathers are issued, so that latency overlaps them — then UNROLL neighbour rows are
+// gathered (one float4 per lane each) before the first add, and added in CSR order.
 template <int LPR, int NV, int UNROLL>
 __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
-    constexpr int GPB = kBlock / LPR;  // groups per block
+    constexpr int GPB = kBlock / LPR;
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
     const int64_t item = int64_t(blockIdx.x) * GPB + g;
-    if (item >= a.n_items) return;  // whole group leaves together
+    if (item >= a.n_items) return;
     const lgcn_item_t it = a.items[item];
     const int64_t d4 = int64_t(LPR) * NV;
-    const float4* __restrict__ xlo = reinterpret_cast<const float4*>(a.x_lo);
-    const float4* __restrict__ xhi = reinterpret_cast<const float4*>(a.x_hi);
-
+    const float4* __restrict__ xlo = reinterpret_cast<const float4*>(a.x_lo) + l;
+    const float4* __restrict__ xhi = reinterpret_cast<const float4*>(a.x_hi) + l;
     float4 acc[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-
+    int cn = 0;
+    float wn = 0.f;
+    if (l < it.len) {
+        cn = *(a.col + it.beg + l);
+        wn = *(a.val + it.beg + l);
+    }
     for (int b = 0; b < it.len; b += LPR) {
         const int n = min(LPR, it.len - b);
-        int c = 0;
-        float w = 0.f;
-        if (l < n) {
-            c = a.col[it.beg + b + l];
-            w = a.val[it.beg + b + l];
+        const int c = cn;
+        const float w = wn;
+        if (b + LPR < it.len && l < it.len - b - LPR) {  // prefetch the next batch
+            cn = *(a.col + it.beg + b + LPR + l);
+            wn = *(a.val + it.beg + b + LPR + l);
         }
         int j = 0;
         for (; j + UNROLL <= n; j += UNROLL) {
@@ -129,10 +140,9 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
             for (int u = 0; u < UNROLL; ++u) {
                 const int cj = __shfl(c, j + u, LPR);
                 wv[u] = __shfl(w, j + u, LPR);
-                const float4* src = (cj < a.x_split) ? xlo + int64_t(cj) * d4
-                                                     : xhi + (int64_t(cj) - a.x_split) * d4;
+                const float4* src = (cj < a.x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - a.x_split) * d4;
 #pragma unroll
-                for (int k = 0; k < NV; ++k) xv[u][k] = src[l + k * LPR];
+                for (int k = 0; k < NV; ++k) xv[u][k] = src[k * LPR];
             }
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u)
@@ -142,95 +152,18 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
         for (; j < n; ++j) {
             const int cj = __shfl(c, j, LPR);
             const float wj = __shfl(w, j, LPR);
-            const float4* src = (cj < a.x_split) ? xlo + int64_t(cj) * d4
-                                                 : xhi + (int64_t(cj) - a.x_split) * d4;
+            const float4* src = (cj < a.x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - a.x_split) * d4;
 #pragma unroll
-            for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wj, src[l + k * LPR]);
+            for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wj, src[k * LPR]);
         }
     }
-
     if (it.dst < 0) {
-        float4* p = reinterpret_cast<float4*>(a.partial) + int64_t(-it.dst - 1) * d4;
+        float4* p = reinterpret_cast<float4*>(a.partial) + int64_t(-it.dst - 1) * d4 + l;
 #pragma unroll
-        for (int k = 0; k < NV; ++k) p[l + k * LPR] = acc[k];
+        for (int k = 0; k < NV; ++k) p[k * LPR] = acc[k];
         return;
     }
     finish_row_vec<LPR, NV>(a, it.dst, l, acc);
-}
-
-// XCD-aware column split: CG column slices of LPRC*NV float4 each. Block b handles slice
-// b % CG of items [(b / CG) * GPB, ...). Workgroups are dealt round-robin over the 8 XCDs, so
-// with CG | 8 every XCD only ever touches one slice of every row and its L2 caches a CG-times
-// smaller working set. Correctness does not depend on placement: every (item, slice) pair is
-// one group. Per-row order and rounding are unchanged (bit-identical to k_spmm_vec).
-template <int LPRC, int NV, int CG, int UNROLL>
-__global__ __launch_bounds__(kBlock) void k_spmm_cs(SpmmArgs a) {
-    constexpr int GPB = kBlock / LPRC;
-    constexpr int BATCH = 16;            // edges per index load round
-    constexpr int R = BATCH / LPRC;      // index registers per lane
-    static_assert(BATCH % LPRC == 0 && BATCH % UNROLL == 0, "batch shape");
-    const int cg = blockIdx.x % CG;
-    const int64_t ib = blockIdx.x / CG;
-    const int g = threadIdx.x / LPRC;
-    const int l = threadIdx.x % LPRC;
-    const int64_t item = ib * GPB + g;
-    if (item >= a.n_items) return;
-    const lgcn_item_t it = a.items[item];
-    const int64_t d4 = a.d / 4;
-    const int base = cg * LPRC * NV;
-    const float4* __restrict__ xlo = reinterpret_cast<const float4*>(a.x_lo) + base + l;
-    const float4* __restrict__ xhi = reinterpret_cast<const float4*>(a.x_hi) + base + l;
-
-    float4 acc[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-
-    for (int b = 0; b < it.len; b += BATCH) {
-        const int n = min(BATCH, it.len - b);
-        int c[R];
-        float w[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int e = l + r * LPRC;
-            c[r] = 0;
-            w[r] = 0.f;
-            if (e < n) {
-                c[r] = a.col[it.beg + b + e];
-                w[r] = a.val[it.beg + b + e];
-            }
-        }
-#pragma unroll
-        for (int j0 = 0; j0 < BATCH; j0 += UNROLL) {
-            if (j0 < n) {
-                float4 xv[UNROLL][NV];
-                float wv[UNROLL];
-#pragma unroll
-                for (int u = 0; u < UNROLL; ++u) {
-                    const int j = j0 + u;
-                    const int cj = __shfl(c[j / LPRC], j % LPRC, LPRC);
-                    wv[u] = __shfl(w[j / LPRC], j % LPRC, LPRC);
-                    const float4* src = (cj < a.x_split) ? xlo + int64_t(cj) * d4
-                                                         : xhi + (int64_t(cj) - a.x_split) * d4;
-#pragma unroll
-                    for (int k = 0; k < NV; ++k)
-                        xv[u][k] = (j < n) ? src[k * LPRC] : make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-#pragma unroll
-                for (int u = 0; u < UNROLL; ++u)
-                    if (j0 + u < n)
-#pragma unroll
-                        for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wv[u], xv[u][k]);
-            }
-        }
-    }
-
-    if (it.dst < 0) {
-        float4* p = reinterpret_cast<float4*>(a.partial) + int64_t(-it.dst - 1) * d4 + base + l;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) p[k * LPRC] = acc[k];
-        return;
-    }
-    finish_row_vec<LPRC, NV>(a, it.dst, base + l, acc);
 }
 
 // Split rows: one workgroup per split row. Group g (of GPB) sums partials g, g+GPB, g+2*GPB, ...
@@ -365,21 +298,6 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass) {
     return LGCN_OK;
 }
 
-template <int LPRC, int NV, int CG, int UNROLL, int LPR_COMBINE, int NV_COMBINE>
-int launch_cs(const SpmmArgs& a, hipStream_t s, int pass) {
-    constexpr int GPB = kBlock / LPRC;
-    if ((pass & PASS_ITEMS) && a.n_items > 0) {
-        const int64_t blocks = (a.n_items + GPB - 1) / GPB * CG;
-        k_spmm_cs<LPRC, NV, CG, UNROLL><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
-        if (int rc = check_launch("k_spmm_cs")) return rc;
-    }
-    if ((pass & PASS_COMBINE) && a.n_splits > 0) {
-        k_combine_vec<LPR_COMBINE, NV_COMBINE><<<dim3(static_cast<unsigned>(a.n_splits)), kBlock, 0, s>>>(a);
-        if (int rc = check_launch("k_combine_vec")) return rc;
-    }
-    return LGCN_OK;
-}
-
 // Kernel-variant override for A/B tuning (LGCN_SPMM_VARIANT; 0 = default choice).
 int spmm_variant() {
     const char* v = std::getenv("LGCN_SPMM_VARIANT");
@@ -456,15 +374,8 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
             case 16: return launch_vec<4, 1, 8>(a, s, pass);
             case 32: return launch_vec<8, 1, 8>(a, s, pass);
             case 64:
-                switch (spmm_variant()) {
-                    case 1: return launch_cs<8, 1, 2, 8, 16, 1>(a, s, pass);   // 2 slices of 128 B
-                    case 2: return launch_cs<4, 1, 4, 8, 16, 1>(a, s, pass);   // 4 slices of 64 B
-                    case 3: return launch_cs<16, 1, 1, 8, 16, 1>(a, s, pass);  // cs code path, 1 slice
-                    case 4: return launch_vec<16, 1, 16>(a, s, pass);          // deeper unroll
-                    case 5: return launch_cs<4, 1, 4, 16, 16, 1>(a, s, pass);
-                    case 6: return launch_cs<8, 1, 2, 16, 16, 1>(a, s, pass);
-                    default: return launch_vec<16, 1, 8>(a, s, pass);
-                }
+                // A/B knob kept for tuning: 1 = 16-deep gather unroll
+                return spmm_variant() == 1 ? launch_vec<16, 1, 16>(a, s, pass) : launch_vec<16, 1, 8>(a, s, pass);
             case 128: return launch_vec<32, 1, 8>(a, s, pass);
             case 256: return launch_vec<64, 1, 8>(a, s, pass);
             case 512: return launch_vec<64, 2, 4>(a, s, pass);

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--chunk", type=int, default=256)
     ap.add_argument("--side", type=int, default=-1, help="side_split (-1 = num_users)")
+    ap.add_argument("--mixed", action="store_true", help="also time the unsided (global longest-first) schedule")
     args = ap.parse_args()
 
     import torch
@@ -37,9 +38,10 @@ def main():
     d, K = args.dim, args.layers
     uw = torch.randn(g.num_users, d, device=dev) * 0.01
     iw = torch.randn(g.num_items, d, device=dev) * 0.01
-    plans = {"mixed": PropagationPlan(ei, g.num_nodes, args.chunk, 0),
-             "sided": PropagationPlan(ei, g.num_nodes, args.chunk, g.num_users if args.side < 0 else args.side)}
-    plan = plans["mixed"]
+    plans = {"sided": PropagationPlan(ei, g.num_nodes, args.chunk, g.num_users if args.side < 0 else args.side)}
+    if args.mixed:
+        plans["mixed"] = PropagationPlan(ei, g.num_nodes, args.chunk, 0)
+    plan = plans["sided"]
     variants = [(int(v), p) for v in args.variants.split(",") for p in plans]
     os.environ["LGCN_SPMM_VARIANT"] = "0"
     ref = lgcn_amd.propagate_forward(uw, iw, plan, K)
