@@ -86,6 +86,12 @@ def load_traffic(workload: str):
         return None
 
 
+def kernel_lpr(d):
+    """Template of the item-pass instance lgcn_spmm launches for width d (csrc/lgcn_spmm.hip)."""
+    return {4: "1,1,8", 8: "2,1,8", 16: "4,1,8", 32: "8,1,8", 64: "16,1,8", 128: "32,1,8", 256: "64,1,8",
+            512: "64,2,4", 1024: "64,4,2"}.get(d, "scalar")
+
+
 def init_dist(backend, dev):
     import torch.distributed as dist
 
@@ -130,8 +136,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--layers", type=int, default=3)
-    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--config", choices=["c2", "c5"], default="c2",
+                    help="propagate workload: c2 = ML-25M-shaped K=3 d=64 (headline); c5 = 10M x 1M x 5e8, K=4 d=256")
+    ap.add_argument("--layers", type=int, default=None, help="K (default 3 for c2, 4 for c5)")
+    ap.add_argument("--dim", type=int, default=None, help="d (default 64 for c2, 256 for c5; train: 128)")
     ap.add_argument("--scale", type=float, default=1.0, help="graph scale vs ML-25M (1.0 = C2)")
     ap.add_argument("--chunk", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -167,13 +175,31 @@ def main():
     if distributed:
         init_dist(args.dist_backend, dev)
 
-    K, d = args.layers, args.dim
+    c5 = args.config == "c5"
+    K = args.layers if args.layers is not None else (4 if c5 else 3)
+    d = args.dim if args.dim is not None else (256 if c5 else 64)
+    d_full = d
     t0 = time.perf_counter()
-    graph = synth.ml25m_shaped(seed=rank, scale=args.scale)
-    log(f"[rank {rank}] graph U={graph.num_users} I={graph.num_items} E={graph.num_edges} "
-        f"{graph.degree_stats()} ({time.perf_counter() - t0:.1f} s)")
-    U, I, N, E = graph.num_users, graph.num_items, graph.num_nodes, graph.num_edges
-    ei = torch.from_numpy(graph.edge_index).to(dev)
+    graph = None
+    if c5:
+        # C5: one synthetic 10M x 1M x 5e8-edge graph (same seed on every rank, generated on the GPU).
+        # N > 1 ranks shard the embedding COLUMNS (feature-sharded propagation): every
+        # rank runs the full plan on d/W columns, no collective; value = K*E / time (strong scaling).
+        s = args.scale
+        U, I = int(synth.C5_USERS * s), int(synth.C5_ITEMS * s)
+        ei = synth.bipartite_device(U, I, int(synth.C5_PAIRS * s), seed=0, device=dev)
+        if d % world or (d // world) % 4:
+            raise SystemExit(f"c5 feature sharding needs d % (4*W) == 0 (d={d}, W={world})")
+        d = d // world
+        N, E = U + I, int(ei.shape[1])
+        log(f"[rank {rank}] c5 graph U={U} I={I} E={E} on device, d={d_full} -> {d} columns per rank "
+            f"({time.perf_counter() - t0:.1f} s)")
+    else:
+        graph = synth.ml25m_shaped(seed=rank, scale=args.scale)
+        log(f"[rank {rank}] graph U={graph.num_users} I={graph.num_items} E={graph.num_edges} "
+            f"{graph.degree_stats()} ({time.perf_counter() - t0:.1f} s)")
+        U, I, N, E = graph.num_users, graph.num_items, graph.num_nodes, graph.num_edges
+        ei = torch.from_numpy(graph.edge_index).to(dev)
     gen = torch.Generator(device=dev).manual_seed(rank)
     user_w = (torch.randn(U, d, device=dev, generator=gen) * 0.01).contiguous()
     item_w = (torch.randn(I, d, device=dev, generator=gen) * 0.01).contiguous()
@@ -219,13 +245,18 @@ def main():
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
         kernel_ms = float(km.item())
 
+    if c5:
+        edges_total = E  # feature-sharded: the ranks together propagate one graph
     value = K * edges_total * args.steps / elapsed
     bytes_per_launch = E * (4 * d + 8) + N * (4 * d + 8)
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    workload = f"C2_ml25m_shaped_K{K}_d{d}" + ("" if args.scale == 1.0 else f"_scale{args.scale}")
+    if c5:
+        workload = f"C5_synthetic_10Mx1M_5e8_K{K}_d{d_full}" + ("" if args.scale == 1.0 else f"_scale{args.scale}")
+    else:
+        workload = f"C2_ml25m_shaped_K{K}_d{d}" + ("" if args.scale == 1.0 else f"_scale{args.scale}")
     traffic = load_traffic(workload)
     result = {
-        "metric": "edges propagated/sec (K=3, d=64)",
+        "metric": f"edges propagated/sec (K={K}, d={d_full})",
         "value": value,
         "unit": "edges/s",
         "n_gpus": world,
@@ -233,20 +264,23 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if c5 else "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (seeded ML-25M-shaped bipartite graph per rank; random N(0,0.01) embeddings)",
-        "config": {"workload": workload, "num_users": U, "num_items": I, "num_edges": E, "layers": K, "dim": d,
-                   "chunk": plan.chunk, "graphs": world,
-                   "parallelism": f"{world} independent graph instance(s), one per GPU, no collective"},
+        "data": ("synthetic (seeded 10M x 1M Zipf bipartite graph generated on device; random N(0,0.01) embeddings)"
+                 if c5 else "synthetic (seeded ML-25M-shaped bipartite graph per rank; random N(0,0.01) embeddings)"),
+        "config": {"workload": workload, "num_users": U, "num_items": I, "num_edges": E, "layers": K, "dim": d_full,
+                   "chunk": plan.chunk, "graphs": 1 if c5 else world,
+                   "parallelism": (f"feature-sharded over {world} GPU(s): {d} columns each, full plan per rank, "
+                                   "no collective") if c5 else
+                                  f"{world} independent graph instance(s), one per GPU, no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_spmm_vec<16,1,8> (lgcn_spmm_items)", "kernel_ms": kernel_ms,
+                     "kernel": f"k_spmm_vec<{kernel_lpr(d)}> (lgcn_spmm_items)", "kernel_ms": kernel_ms,
                      "bytes_per_launch": bytes_per_launch},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not c5:
         result["cpu_baseline"] = cpu_baseline(graph, K, d)
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -279,8 +313,8 @@ def run_train(args):
     torch.cuda.set_device(dev)
     if world > 1:
         init_dist(args.dist_backend, dev)
-    K = args.layers
-    d = args.dim if args.dim != 64 else 128
+    K = args.layers if args.layers is not None else 3
+    d = args.dim if args.dim is not None else 128
     t0 = time.perf_counter()
     g = synth.ml25m_shaped(seed=0, scale=args.scale)  # one graph, replicated tables (DP)
     U, I, N = g.num_users, g.num_items, g.num_nodes

@@ -87,3 +87,55 @@ def ml25m_shaped(seed: int = 0, scale: float = 1.0) -> BipartiteGraph:
     I = max(2, int(ML25M_ITEMS * scale))
     P = max(1, int(ML25M_PAIRS * scale))
     return bipartite(U, I, P, seed)
+
+
+def bipartite_device(num_users: int, num_items: int, num_pairs: int, seed: int = 0, device="cuda",
+                     user_alpha: float = 0.75, user_offset: float = 40.0, item_alpha: float = 1.0,
+                     item_offset: float = 12.0):
+    """The same Zipf-like user/item draw as ``random_pairs`` but generated on the device with torch
+    (for C5-sized graphs: 5e8 edges would need tens of GB of host RAM in numpy). Returns the
+    coalesced undirected edge_index [2, E] (int64, on ``device``). Not bit-identical to the numpy
+    generator (different RNG); seeded and deterministic for a given device type."""
+    import torch
+
+    dev = torch.device(device)
+    g = torch.Generator(device=dev).manual_seed(seed)
+
+    def weights(n, alpha, offset):
+        w = 1.0 / torch.pow(torch.arange(1, n + 1, device=dev, dtype=torch.float64) + offset, alpha)
+        w = w[torch.randperm(n, device=dev, generator=g)]
+        return (w / w.sum()).to(torch.float32)
+
+    pu = weights(num_users, user_alpha, user_offset)
+    pi = weights(num_items, item_alpha, item_offset)
+    cu = torch.cumsum(pu.double(), 0)
+    ci = torch.cumsum(pi.double(), 0)
+    keys = torch.empty(0, dtype=torch.int64, device=dev)
+    draw = int(num_pairs * 1.3) + 1024
+    for _ in range(12):
+        ru = torch.rand(draw, device=dev, generator=g, dtype=torch.float64) * cu[-1]
+        ri = torch.rand(draw, device=dev, generator=g, dtype=torch.float64) * ci[-1]
+        u = torch.searchsorted(cu, ru).clamp_(max=num_users - 1)
+        it = torch.searchsorted(ci, ri).clamp_(max=num_items - 1)
+        del ru, ri
+        keys = torch.unique(torch.cat([keys, u * num_items + it]))
+        del u, it
+        if keys.numel() >= num_pairs:
+            break
+        draw = int((num_pairs - keys.numel()) * 2.0) + 1024
+    if keys.numel() > num_pairs:
+        pick = torch.randperm(keys.numel(), device=dev, generator=g)[:num_pairs]
+        keys = torch.sort(keys[pick]).values
+    N = num_users + num_items
+    users = keys // num_items
+    items = keys % num_items + num_users
+    del keys
+    key = torch.cat([users * N + items, items * N + users])
+    del users, items
+    key = torch.sort(key).values  # unique already: (u, i) pairs are distinct and directions disjoint
+    return torch.stack([key // N, key % N])
+
+
+C5_USERS = 10_000_000
+C5_ITEMS = 1_000_000
+C5_PAIRS = 250_000_000
