@@ -149,6 +149,7 @@ def main():
     ap.add_argument("--parts-per-batch", type=int, default=32, help="train: parts per step")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for runs; gloo to rehearse N ranks on one GPU")
     ap.add_argument("--torch-adam", action="store_true", help="train: torch Adam + clip_grad_norm_ (reference ops)")
+    ap.add_argument("--no-graphs", action="store_true", help="train: run the fused step eagerly (no hipGraph replay)")
     ap.add_argument("--autograd", action="store_true",
                     help="train: reference-style step (compute_embeddings + bpr_loss + autograd) instead of "
                          "the fused no-autograd step")
@@ -341,7 +342,8 @@ def run_train(args):
     else:
         from lgcn_amd.optim import FusedAdam
 
-        opt = FusedAdam(model.parameters(), lr=1e-3, max_grad_norm=1)
+        opt = FusedAdam(model.parameters(), lr=1e-3, max_grad_norm=1, capturable=not args.autograd,
+                        keep_clipped_grad=False)
     params = list(model.parameters())
     torch.manual_seed(1000 + rank)
 
@@ -349,7 +351,7 @@ def run_train(args):
     if not args.autograd:
         from lgcn_amd.train_step import FusedTrainStep
 
-        fused = FusedTrainStep(model, opt, world=world)
+        fused = FusedTrainStep(model, opt, world=world, graphs=not args.no_graphs and not args.torch_adam)
 
     def step(bidx):
         batch = batches[bidx]
@@ -393,7 +395,8 @@ def run_train(args):
         "data": "synthetic (seeded ML-25M-shaped graph, 90/5/5 directed split)",
         "config": {"workload": f"C{3 if world == 1 else 4}_cluster_gcn_train", "parts": args.parts,
                    "optimizer": "torch Adam + clip_grad_norm_" if args.torch_adam else "lgcn FusedAdam (clip fused)",
-                   "step": "autograd (reference ops)" if args.autograd else "fused (lgcn_bpr_fused + sorted scatter)",
+                   "step": "autograd (reference ops)" if args.autograd else
+                           ("fused sparse step" + ("" if (args.no_graphs or args.torch_adam) else ", hipGraph per batch")),
                    "parts_per_batch": q, "f_intra": f_intra, "layers": K, "dim": d, "num_users": U,
                    "num_items": I, "train_edges": n_tr,
                    "parallelism": f"dp{world}: disjoint part batches per rank, RCCL all_reduce of embedding grads"},

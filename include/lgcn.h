@@ -69,6 +69,7 @@ typedef struct {
  *   FINAL_ACC : acc[r] = ((acc[r] + v) / div) * mul
  *   FINAL_E   : acc[r] = ((e[r]  + v) / div) * mul
  *   STORE     : acc[r] = v   (a bare LGConv layer)
+ *   SCALE     : acc[r] = (v * mul) / div   (the backward seed from summed gradient rows)
  * LightGCN forward with K layers (reference models/light_gcn.py:29-36):
  *   layer 1 INIT(e=x0), layers 2..K-1 ADD, layer K FINAL_ACC(div=K+1, mul=fp32(1/(K+1)));
  *   K == 1 uses FINAL_E(e=x0).
@@ -79,7 +80,8 @@ enum {
     LGCN_EPI_ADD = 1,
     LGCN_EPI_FINAL_ACC = 2,
     LGCN_EPI_FINAL_E = 3,
-    LGCN_EPI_STORE = 4
+    LGCN_EPI_STORE = 4,
+    LGCN_EPI_SCALE = 5
 };
 
 const char* lgcn_last_error(void);
@@ -120,12 +122,15 @@ int lgcn_edge_norm(const int64_t* rowptr, const int32_t* col, int64_t N, int64_t
  * side_split = num_users, so the rows gathering from the item table run together and then the
  * rows gathering from the user table: each phase has one table's working set in L2); inside a
  * side items are ordered longest-first (stable), so neighbouring lane groups of a wave carry
- * equal work. side_split = 0 gives one global longest-first order. Capacities: items <= N + E/chunk, splits <= N,
+ * equal work. side_split = 0 gives one global longest-first order. row_mask (device uint8[N],
+ * nullable) restricts the schedule to rows with row_mask[r] != 0: rows outside it get no item, so
+ * lgcn_spmm leaves them untouched (the sparse Cluster-GCN batch step schedules only the rows its
+ * edges touch). Capacities: items <= N + E/chunk, splits <= N,
  * partials <= E/chunk + N. counts[0..2] (device int64) receive n_items, n_splits,
  * n_partials; the caller reads them back once per plan. */
 int lgcn_schedule_workspace_size(int64_t E, int64_t N, int32_t chunk, size_t* bytes);
 int lgcn_schedule_build(const int64_t* rowptr, int64_t N, int64_t E, int32_t chunk,
-                        int64_t side_split, lgcn_item_t* items, int64_t items_cap,
+                        int64_t side_split, const uint8_t* row_mask, lgcn_item_t* items, int64_t items_cap,
                         lgcn_split_t* splits, int64_t splits_cap,
                         int64_t* counts, void* ws, size_t ws_bytes, lgcn_stream_t stream);
 
@@ -137,8 +142,8 @@ int lgcn_schedule_build(const int64_t* rowptr, int64_t N, int64_t E, int32_t chu
  * x: split table (gather source). e: split table (epilogue addend; may be NULL unless the
  * mode reads it). acc: split table (accumulator / final output). y: optional [N,d] layer
  * output (input of the next layer). partial: [n_partials, d] scratch.
- * Rows with no item still get nothing written: every row of the plan has at least one
- * item (zero-length for zero in-degree), so the epilogue covers all N rows. */
+ * Every row of an unmasked plan has at least one item (zero-length for zero in-degree), so the
+ * epilogue covers all N rows; a row_mask plan writes only its rows. */
 int lgcn_spmm(const lgcn_item_t* items, int64_t n_items,
               const lgcn_split_t* splits, int64_t n_splits,
               const int32_t* col, const float* val, int64_t N, int32_t d,
@@ -187,17 +192,46 @@ int lgcn_copy_scale(const float* x_lo, const float* x_hi, int64_t x_split, int64
  *   lgcn_bpr_fused writes, per triplet, dF rows cf[b], cf[B+b], cf[2B+b] (d loss / d F rows of
  *   u, p, n), reg-gradient rows cw[...] (d loss / d W rows) and terms[b] = softplus term,
  *   terms[B+b] = sum of squares of the three W rows. d in {16,32,64,128,256,512}.
+ *   touched (device uint8[N], nullable): rows with touched[r] == 0 were not propagated (a sparse
+ *   batch plan) and their F row is (W[r] / div) * mul — LightGCN's output for a row no batch edge
+ *   reaches (every layer adds an exact 0).
  *   lgcn_bpr_loss: loss[0] = -(mean softplus)/10 + coeff * sum(squares)/(B*d).
  *   lgcn_segment_rows: out[r] (+)= sum of C[perm[e]] for e in [rowptr[r], rowptr[r+1]) in order —
  *   the deterministic scatter of those rows, with rowptr/perm from lgcn_csr_build over the 3B keys
- *   (u, U+p, U+n). add == 0 writes every row (0 where empty); add != 0 only adds. */
+ *   (u, U+p, U+n). add == 0 writes every row as (sum * mul) / div (0 where empty) — with the
+ *   LightGCN backward scale this is the seed g of the backward; add != 0 only adds (sum * mul) / div
+ *   to rows with contributions. */
 int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split,
                    const float* w_lo, const float* w_hi, int64_t w_split, int64_t U,
                    const int64_t* u, const int64_t* p, const int64_t* n, int64_t B, int32_t d,
+                   const uint8_t* touched, float div, float mul,
                    float coeff, float* cf, float* cw, float* terms, lgcn_stream_t stream);
 int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* loss, lgcn_stream_t stream);
 int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C, int64_t N, int32_t d,
-                      float* out_lo, float* out_hi, int64_t split, int32_t add, lgcn_stream_t stream);
+                      float* out_lo, float* out_hi, int64_t split, int32_t add, float mul, float div,
+                      lgcn_stream_t stream);
+/* The per-step part of that scatter for the B random negatives, without a general sort:
+ *   lgcn_sort_keys_small: one workgroup sorts (keys[b] + key_offset, b) pairs (B <= 16384) into
+ *     sorted[] (uint64 = row << 32 | b);
+ *   lgcn_sorted_segment_add: out[row] += (sum of C[b] over the run of equal rows, in b order)
+ *     * mul / div. (The users/positives part has a fixed structure per batch and goes through a
+ *     load-balanced plan built once, with lgcn_spmm SCALE / ADD epilogues.) */
+int lgcn_sort_keys_small(const int64_t* keys, int64_t B, int64_t key_offset, uint64_t* sorted, lgcn_stream_t stream);
+/* Same result as sort + sorted_segment_add in ONE launch: out[key_offset + keys[b]] += (sum over b,
+ * in b order, of C[b]) * mul / div for keys in [0, nrows). Workgroup w owns a key range and keeps
+ * its keys in b order by an ordered block compaction; used for the per-step negatives.
+ * Optional second source C2 (nullable): the same per-row sums of C2 are parked in c2buf[b_first]
+ * (c2flag[b_first] = 1; the launch clears c2flag) for lgcn_flagged_rows_add to add LATER (the
+ * negatives' reg-gradient rows must land after the backward). *overflow (nullable, caller-zeroed)
+ * is set if a workgroup's list overflowed — parked sums would then be split; callers check it. */
+int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
+                           int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
+                           const float* C2, float* c2buf, uint8_t* c2flag, int32_t* overflow, lgcn_stream_t stream);
+int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, const float* c2buf,
+                          const uint8_t* c2flag, int32_t d, float* out_lo, float* out_hi, int64_t split,
+                          lgcn_stream_t stream);
+int lgcn_sorted_segment_add(const uint64_t* sorted, int64_t B, const float* C, int32_t d, float* out_lo,
+                            float* out_hi, int64_t split, float mul, float div, lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Training-step tail (reference utils/train_test.py:95-96: clip_grad_norm_(max_norm=1) then
@@ -222,7 +256,11 @@ int lgcn_grad_norm(const lgcn_adam_tensor_t* tensors, int32_t n, float max_norm,
                    lgcn_stream_t stream);
 int lgcn_adam_step(const lgcn_adam_tensor_t* tensors, int32_t n, float one_minus_beta1, float beta2,
                    float one_minus_beta2, float eps, float step_size, float bc2_sqrt, const float* clip,
-                   int32_t write_grad, lgcn_stream_t stream);
+                   const float* dev_scalars, int32_t write_grad, lgcn_stream_t stream);
+/* Capturable form: lgcn_adam_prologue advances a device step counter (double) and writes
+ * scalars[0] = -lr/(1-b1^t), scalars[1] = sqrt(1-b2^t); pass scalars as dev_scalars to
+ * lgcn_adam_step (its step_size / bc2_sqrt arguments are then ignored). */
+int lgcn_adam_prologue(double* step, float lr, double beta1, double beta2, float* scalars, lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Host-side (no GPU): balanced k-way node partition for Cluster-GCN batching, the METIS

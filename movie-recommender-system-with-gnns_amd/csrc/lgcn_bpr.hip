@@ -48,6 +48,9 @@ struct BprArgs {
     const int64_t* n;
     int64_t B;
     int32_t d;
+    const uint8_t* touched;  // nullable: rows not propagated use (W / div) * mul
+    float div;
+    float mul;
     float coeff;
     float* cf;     // [3B, d] dF rows (u | p | n)
     float* cw;     // [3B, d] reg-gradient rows for W (u | p | n)
@@ -65,12 +68,16 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
     const int64_t ru = a.u[b];
     const int64_t rp = a.U + a.p[b];
     const int64_t rn = a.U + a.n[b];
-    const float4* fu = reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, ru, d)) + l;
-    const float4* fp = reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, rp, d)) + l;
-    const float4* fn = reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, rn, d)) + l;
     const float4* wu = reinterpret_cast<const float4*>(srow(a.w_lo, a.w_hi, a.w_split, ru, d)) + l;
     const float4* wp = reinterpret_cast<const float4*>(srow(a.w_lo, a.w_hi, a.w_split, rp, d)) + l;
     const float4* wn = reinterpret_cast<const float4*>(srow(a.w_lo, a.w_hi, a.w_split, rn, d)) + l;
+    // a row the sparse batch never reached is (x0 / div) * mul: read it from W instead of F
+    const bool tu = a.touched == nullptr || a.touched[ru];
+    const bool tp = a.touched == nullptr || a.touched[rp];
+    const bool tn = a.touched == nullptr || a.touched[rn];
+    const float4* fu = tu ? reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, ru, d)) + l : wu;
+    const float4* fp = tp ? reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, rp, d)) + l : wp;
+    const float4* fn = tn ? reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, rn, d)) + l : wn;
     float4 U_[NV], P_[NV], N_[NV], WU[NV], WP[NV], WN[NV];
     float suu = 0.f, spp = 0.f, snn = 0.f, sup = 0.f, sun = 0.f, sreg = 0.f;
 #pragma unroll
@@ -78,6 +85,9 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
         U_[k] = fu[k * LPR];
         P_[k] = fp[k * LPR];
         N_[k] = fn[k * LPR];
+        if (!tu) U_[k] = make_float4((U_[k].x / a.div) * a.mul, (U_[k].y / a.div) * a.mul, (U_[k].z / a.div) * a.mul, (U_[k].w / a.div) * a.mul);
+        if (!tp) P_[k] = make_float4((P_[k].x / a.div) * a.mul, (P_[k].y / a.div) * a.mul, (P_[k].z / a.div) * a.mul, (P_[k].w / a.div) * a.mul);
+        if (!tn) N_[k] = make_float4((N_[k].x / a.div) * a.mul, (N_[k].y / a.div) * a.mul, (N_[k].z / a.div) * a.mul, (N_[k].w / a.div) * a.mul);
         WU[k] = wu[k * LPR];
         WP[k] = wp[k * LPR];
         WN[k] = wn[k * LPR];
@@ -137,9 +147,11 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_bpr_loss(const float* __restrict__ terms, int64_t B, int32_t d,
-                                                     float coeff, float* __restrict__ loss) {
-    __shared__ float r0[kBlock / 64], r1[kBlock / 64];
+constexpr int kLossBlock = 1024;
+
+__global__ __launch_bounds__(kLossBlock) void k_bpr_loss(const float* __restrict__ terms, int64_t B, int32_t d,
+                                                         float coeff, float* __restrict__ loss) {
+    __shared__ float r0[kLossBlock / 64], r1[kLossBlock / 64];
     float s0 = 0.f, s1 = 0.f;
     for (int64_t i = threadIdx.x; i < B; i += blockDim.x) {
         s0 += terms[i];
@@ -156,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void k_bpr_loss(const float* __restrict__ t
     __syncthreads();
     if (threadIdx.x == 0) {
         float a = 0.f, c = 0.f;
-        for (int w = 0; w < kBlock / 64; ++w) {
+        for (int w = 0; w < kLossBlock / 64; ++w) {
             a += r0[w];
             c += r1[w];
         }
@@ -172,7 +184,8 @@ template <int LPR, int NV>
 __global__ __launch_bounds__(kBlock) void k_segment_rows(const int64_t* __restrict__ rowptr,
                                                          const int32_t* __restrict__ perm,
                                                          const float* __restrict__ C, int64_t N, int32_t d,
-                                                         float* out_lo, float* out_hi, int64_t split, int add) {
+                                                         float* out_lo, float* out_hi, int64_t split, int add,
+                                                         float mul, float div) {
     constexpr int GPB = kBlock / LPR;
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
@@ -196,10 +209,281 @@ __global__ __launch_bounds__(kBlock) void k_segment_rows(const int64_t* __restri
     for (int k = 0; k < NV; ++k) {
         if (add) {
             const float4 v = o[k * LPR];
-            acc[k] = make_float4(v.x + acc[k].x, v.y + acc[k].y, v.z + acc[k].z, v.w + acc[k].w);
+            acc[k] = make_float4(v.x + (acc[k].x * mul) / div, v.y + (acc[k].y * mul) / div,
+                                 v.z + (acc[k].z * mul) / div, v.w + (acc[k].w * mul) / div);
+        } else {
+            acc[k] = make_float4((acc[k].x * mul) / div, (acc[k].y * mul) / div, (acc[k].z * mul) / div,
+                                 (acc[k].w * mul) / div);
         }
         o[k * LPR] = acc[k];
     }
+}
+
+// ---- per-step scatter of the negatives' gradient rows (deterministic, no atomics) ----
+constexpr int kSmallSort = 16384;
+
+// One workgroup bitonic-sorts B <= 16384 packed (row << 32 | index) words in LDS; equal rows
+// keep index order (the index is the low word), so each row's contributions come out in a fixed
+// order whatever the scheduling.
+__global__ __launch_bounds__(1024) void k_sort_small(const int64_t* __restrict__ keys, int64_t B, int64_t key_offset,
+                                                     unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long sh[kSmallSort];
+    int P = 1;
+    while (P < B) P <<= 1;
+    for (int i = threadIdx.x; i < P; i += blockDim.x)
+        sh[i] = (i < B) ? ((static_cast<unsigned long long>(keys[i] + key_offset) << 32) | static_cast<unsigned>(i))
+                        : ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long a = sh[i], b = sh[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        sh[i] = b;
+                        sh[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < B; i += blockDim.x) out[i] = sh[i];
+}
+
+// One lane group per sorted position; the head of each run of equal rows sums the run's C rows
+// in index order and adds (sum * mul) / div into its output row.
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_sorted_segment_add(const unsigned long long* __restrict__ sorted, int64_t B,
+                                                               const float* __restrict__ C, int32_t d, float* out_lo,
+                                                               float* out_hi, int64_t split, float mul, float div) {
+    constexpr int GPB = kBlock / LPR;
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    const int64_t j = int64_t(blockIdx.x) * GPB + g;
+    if (j >= B) return;
+    const unsigned long long w = sorted[j];
+    const int64_t row = static_cast<int64_t>(w >> 32);
+    if (j > 0 && static_cast<int64_t>(sorted[j - 1] >> 32) == row) return;
+    float4 acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t e = j; e < B; ++e) {
+        const unsigned long long we = sorted[e];
+        if (static_cast<int64_t>(we >> 32) != row) break;
+        const float4* c = reinterpret_cast<const float4*>(C + int64_t(static_cast<unsigned>(we)) * d) + l;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const float4 v = c[k * LPR];
+            acc[k] = make_float4(acc[k].x + v.x, acc[k].y + v.y, acc[k].z + v.z, acc[k].w + v.w);
+        }
+    }
+    float4* o = reinterpret_cast<float4*>(srow(out_lo, out_hi, split, row, int64_t(d))) + l;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const float4 v = o[k * LPR];
+        o[k * LPR] = make_float4(v.x + (acc[k].x * mul) / div, v.y + (acc[k].y * mul) / div,
+                                 v.z + (acc[k].z * mul) / div, v.w + (acc[k].w * mul) / div);
+    }
+}
+
+// Range-owner scatter: workgroup w owns output rows [key_offset + w*span, ... + span). It streams
+// all B keys in index order, keeps the ones in its range through an ORDERED block compaction
+// (wave ballot + per-wave prefix), so its list is in b order, then every first occurrence of a row
+// sums that row's C rows in list (= b) order and adds (sum * mul) / div to it. One launch,
+// deterministic, no atomics; each workgroup reads the B keys once (L2-resident).
+constexpr int kRangeCap = 4096;
+
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_range_scatter(const int64_t* __restrict__ keys, int64_t B, int64_t nrows,
+                                                          int64_t span, int64_t key_offset, const float* __restrict__ C,
+                                                          int32_t d, float* out_lo, float* out_hi, int64_t split,
+                                                          float mul, float div, const float* __restrict__ C2,
+                                                          float* __restrict__ c2buf, uint8_t* __restrict__ c2flag,
+                                                          int* __restrict__ overflow) {
+    constexpr int GPB = kBlock / LPR;
+    __shared__ int lkey[kRangeCap];
+    __shared__ int lidx[kRangeCap];
+    __shared__ int wave_cnt[kBlock / 64];
+    __shared__ int list_n;
+    const int64_t lo = int64_t(blockIdx.x) * span;
+    const int64_t hi = lo + span < nrows ? lo + span : nrows;
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    if (threadIdx.x == 0) list_n = 0;
+    __syncthreads();
+    int64_t base = 0;
+    constexpr int KPT = 16;  // keys per thread per round: thread t owns b = base + t*KPT + j
+    while (true) {
+        // fill the list (ordered) until full or all keys seen
+        for (; base < B; base += int64_t(kBlock) * KPT) {
+            int c = 0;
+            unsigned short hit = 0;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const int64_t bj = base + int64_t(threadIdx.x) * KPT + j;
+                if (bj < B) {
+                    const int64_t key = keys[bj];
+                    if (key >= lo && key < hi) {
+                        hit |= static_cast<unsigned short>(1u << j);
+                        ++c;
+                    }
+                }
+            }
+            // ordered block-wide exclusive scan of c (thread order == b order)
+            int incl = c;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int v = __shfl_up(incl, off, 64);
+                if (lane >= off) incl += v;
+            }
+            if (lane == 63) wave_cnt[wv] = incl;
+            __syncthreads();
+            int off = list_n;
+            for (int w = 0; w < wv; ++w) off += wave_cnt[w];
+            off += incl - c;
+            int total = list_n;
+            for (int w = 0; w < kBlock / 64; ++w) total += wave_cnt[w];
+            if (total > kRangeCap) {  // this round does not fit: flush first, redo it
+                if (threadIdx.x == 0 && overflow) *overflow = 1;  // C2 rows would then be split: report
+                __syncthreads();
+                break;
+            }
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                if (hit & (1u << j)) {
+                    const int64_t bj = base + int64_t(threadIdx.x) * KPT + j;
+                    lkey[off] = static_cast<int>(keys[bj] - lo);
+                    lidx[off] = static_cast<int>(bj);
+                    ++off;
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) list_n = total;
+            __syncthreads();
+        }
+        // sum every row of the list in list order
+        const int n = list_n;
+        for (int e = g; e < n; e += GPB) {
+            const int key = lkey[e];
+            bool first = true;
+            for (int q = 0; q < e; ++q)
+                if (lkey[q] == key) {
+                    first = false;
+                    break;
+                }
+            if (!first) continue;
+            float4 acc[NV], acc2[NV];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {
+                acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                acc2[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            for (int q = e; q < n; ++q) {
+                if (lkey[q] != key) continue;
+                const float4* c = reinterpret_cast<const float4*>(C + int64_t(lidx[q]) * d) + l;
+#pragma unroll
+                for (int k = 0; k < NV; ++k) {
+                    const float4 v = c[k * LPR];
+                    acc[k] = make_float4(acc[k].x + v.x, acc[k].y + v.y, acc[k].z + v.z, acc[k].w + v.w);
+                }
+                if (C2) {
+                    const float4* c2 = reinterpret_cast<const float4*>(C2 + int64_t(lidx[q]) * d) + l;
+#pragma unroll
+                    for (int k = 0; k < NV; ++k) {
+                        const float4 v = c2[k * LPR];
+                        acc2[k] = make_float4(acc2[k].x + v.x, acc2[k].y + v.y, acc2[k].z + v.z, acc2[k].w + v.w);
+                    }
+                }
+            }
+            if (C2) {  // second source: park the row's sum in the slot of its first occurrence
+                float4* cb = reinterpret_cast<float4*>(c2buf + int64_t(lidx[e]) * d) + l;
+#pragma unroll
+                for (int k = 0; k < NV; ++k) cb[k * LPR] = acc2[k];
+                if (l == 0) c2flag[lidx[e]] = 1;
+            }
+            const int64_t row = lo + key + key_offset;
+            float4* o = reinterpret_cast<float4*>(srow(out_lo, out_hi, split, row, int64_t(d))) + l;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {
+                const float4 v = o[k * LPR];
+                o[k * LPR] = make_float4(v.x + (acc[k].x * mul) / div, v.y + (acc[k].y * mul) / div,
+                                         v.z + (acc[k].z * mul) / div, v.w + (acc[k].w * mul) / div);
+            }
+        }
+        __syncthreads();
+        if (base >= B) break;
+        if (threadIdx.x == 0) list_n = 0;
+        __syncthreads();
+    }
+}
+
+// Second pass for the parked sums: each flagged slot b adds c2buf[b] to row keys[b] + key_offset.
+// Every row owns at most one flagged slot (its first occurrence) unless the scatter overflowed.
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_flagged_rows_add(const int64_t* __restrict__ keys, int64_t B,
+                                                             int64_t key_offset, const float* __restrict__ c2buf,
+                                                             const uint8_t* __restrict__ c2flag, int32_t d,
+                                                             float* out_lo, float* out_hi, int64_t split) {
+    constexpr int GPB = kBlock / LPR;
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    const int64_t b = int64_t(blockIdx.x) * GPB + g;
+    if (b >= B || !c2flag[b]) return;
+    const float4* c = reinterpret_cast<const float4*>(c2buf + b * d) + l;
+    float4* o = reinterpret_cast<float4*>(srow(out_lo, out_hi, split, keys[b] + key_offset, int64_t(d))) + l;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const float4 v = o[k * LPR], a = c[k * LPR];
+        o[k * LPR] = make_float4(v.x + a.x, v.y + a.y, v.z + a.z, v.w + a.w);
+    }
+}
+
+template <int LPR, int NV>
+int launch_rs(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C, int32_t d, float* lo,
+              float* hi, int64_t split, float mul, float div, const float* C2, float* c2buf, uint8_t* c2flag,
+              int* overflow, hipStream_t s) {
+    // every workgroup streams all B keys once; enough workgroups that each keeps ~<= 256 entries
+    // on average (the list holds kRangeCap), at least 256 (one per CU)
+    int64_t wgs = B / 256 + 1;
+    if (wgs < 256) wgs = 256;
+    if (wgs > 65535) wgs = 65535;
+    if (wgs > nrows) wgs = nrows > 0 ? nrows : 1;
+    const int64_t span = (nrows + wgs - 1) / wgs;
+    const int64_t grid = (nrows + span - 1) / span;
+    if (C2) {
+        if (int rc = check_hip(hipMemsetAsync(c2flag, 0, static_cast<size_t>(B), s), "memset c2flag")) return rc;
+    }
+    k_range_scatter<LPR, NV><<<dim3(static_cast<unsigned>(grid)), kBlock, 0, s>>>(keys, B, nrows, span, key_offset, C, d,
+                                                                                 lo, hi, split, mul, div, C2, c2buf,
+                                                                                 c2flag, overflow);
+    return check_launch("k_range_scatter");
+}
+
+template <int LPR, int NV>
+int launch_fra(const int64_t* keys, int64_t B, int64_t key_offset, const float* c2buf, const uint8_t* c2flag, int32_t d,
+               float* lo, float* hi, int64_t split, hipStream_t s) {
+    constexpr int GPB = kBlock / LPR;
+    const int64_t blocks = (B + GPB - 1) / GPB;
+    if (blocks > 0)
+        k_flagged_rows_add<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(keys, B, key_offset, c2buf,
+                                                                                         c2flag, d, lo, hi, split);
+    return check_launch("k_flagged_rows_add");
+}
+
+template <int LPR, int NV>
+int launch_ssa(const unsigned long long* sorted, int64_t B, const float* C, int32_t d, float* lo, float* hi,
+               int64_t split, float mul, float div, hipStream_t s) {
+    constexpr int GPB = kBlock / LPR;
+    const int64_t blocks = (B + GPB - 1) / GPB;
+    if (blocks > 0)
+        k_sorted_segment_add<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(sorted, B, C, d, lo, hi,
+                                                                                           split, mul, div);
+    return check_launch("k_sorted_segment_add");
 }
 
 template <int LPR, int NV>
@@ -212,11 +496,11 @@ int launch_bpr(const BprArgs& a, hipStream_t s) {
 
 template <int LPR, int NV>
 int launch_seg(const int64_t* rowptr, const int32_t* perm, const float* C, int64_t N, int32_t d, float* lo, float* hi,
-               int64_t split, int add, hipStream_t s) {
+               int64_t split, int add, float mul, float div, hipStream_t s) {
     constexpr int GPB = kBlock / LPR;
     const int64_t blocks = (N + GPB - 1) / GPB;
     k_segment_rows<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(rowptr, perm, C, N, d, lo, hi,
-                                                                                  split, add);
+                                                                                  split, add, mul, div);
     return check_launch("k_segment_rows");
 }
 
@@ -228,7 +512,8 @@ extern "C" {
 
 int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split, const float* w_lo, const float* w_hi,
                    int64_t w_split, int64_t U, const int64_t* u, const int64_t* p, const int64_t* n, int64_t B,
-                   int32_t d, float coeff, float* cf, float* cw, float* terms, lgcn_stream_t stream) {
+                   int32_t d, const uint8_t* touched, float div, float mul, float coeff, float* cf, float* cw,
+                   float* terms, lgcn_stream_t stream) {
     if (B < 0 || d <= 0 || U < 0) return fail(LGCN_E_ARG, "lgcn_bpr_fused: bad sizes");
     if (B == 0) return LGCN_OK;
     if (!f_lo || !w_lo || !u || !p || !n || !cf || !cw || !terms)
@@ -236,7 +521,7 @@ int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split, const 
     if (d % 4 != 0 || !al16(f_lo) || !al16(w_lo) || (f_hi && !al16(f_hi)) || (w_hi && !al16(w_hi)) || !al16(cf) ||
         !al16(cw))
         return fail(LGCN_E_UNSUPPORTED, "lgcn_bpr_fused: needs d %% 4 == 0 and 16-byte aligned rows (d=%d)", d);
-    BprArgs a{f_lo, f_hi, f_split, w_lo, w_hi, w_split, U, u, p, n, B, d, coeff, cf, cw, terms};
+    BprArgs a{f_lo, f_hi, f_split, w_lo, w_hi, w_split, U, u, p, n, B, d, touched, div, mul, coeff, cf, cw, terms};
     hipStream_t s = as_stream(stream);
     switch (d) {
         case 16: return launch_bpr<4, 1>(a, s);
@@ -249,26 +534,95 @@ int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split, const 
     }
 }
 
+int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
+                           int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
+                           const float* C2, float* c2buf, uint8_t* c2flag, int32_t* overflow, lgcn_stream_t stream) {
+    if (B < 0 || d <= 0 || nrows < 0 || (B > 0 && (!keys || !C || !out_lo)) || (C2 && (!c2buf || !c2flag)))
+        return fail(LGCN_E_ARG, "lgcn_range_scatter_add: bad args");
+    if (B == 0 || nrows == 0) return LGCN_OK;
+    if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C2 && (!al16(C2) || !al16(c2buf))))
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_range_scatter_add: needs d %% 4 == 0 and aligned rows");
+    hipStream_t s = as_stream(stream);
+#define LGCN_RS(L, V) launch_rs<L, V>(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, c2buf, c2flag, overflow, s)
+    switch (d) {
+        case 16: return LGCN_RS(4, 1);
+        case 32: return LGCN_RS(8, 1);
+        case 64: return LGCN_RS(16, 1);
+        case 128: return LGCN_RS(32, 1);
+        case 256: return LGCN_RS(64, 1);
+        case 512: return LGCN_RS(64, 2);
+        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_range_scatter_add: d=%d", d);
+    }
+#undef LGCN_RS
+}
+
+int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, const float* c2buf, const uint8_t* c2flag,
+                          int32_t d, float* out_lo, float* out_hi, int64_t split, lgcn_stream_t stream) {
+    if (B < 0 || d <= 0 || (B > 0 && (!keys || !c2buf || !c2flag || !out_lo))) return fail(LGCN_E_ARG, "lgcn_flagged_rows_add: bad args");
+    if (B == 0) return LGCN_OK;
+    hipStream_t s = as_stream(stream);
+#define LGCN_FRA(L, V) launch_fra<L, V>(keys, B, key_offset, c2buf, c2flag, d, out_lo, out_hi, split, s)
+    switch (d) {
+        case 16: return LGCN_FRA(4, 1);
+        case 32: return LGCN_FRA(8, 1);
+        case 64: return LGCN_FRA(16, 1);
+        case 128: return LGCN_FRA(32, 1);
+        case 256: return LGCN_FRA(64, 1);
+        case 512: return LGCN_FRA(64, 2);
+        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_flagged_rows_add: d=%d", d);
+    }
+#undef LGCN_FRA
+}
+
+int lgcn_sort_keys_small(const int64_t* keys, int64_t B, int64_t key_offset, uint64_t* sorted, lgcn_stream_t stream) {
+    if (B < 0 || B > kSmallSort || (B > 0 && (!keys || !sorted)))
+        return fail(LGCN_E_ARG, "lgcn_sort_keys_small: B=%lld (max %d)", (long long)B, kSmallSort);
+    if (B == 0) return LGCN_OK;
+    k_sort_small<<<1, 1024, 0, as_stream(stream)>>>(keys, B, key_offset,
+                                                    reinterpret_cast<unsigned long long*>(sorted));
+    return check_launch("k_sort_small");
+}
+
+int lgcn_sorted_segment_add(const uint64_t* sorted, int64_t B, const float* C, int32_t d, float* out_lo,
+                            float* out_hi, int64_t split, float mul, float div, lgcn_stream_t stream) {
+    if (B < 0 || d <= 0 || (B > 0 && (!sorted || !C || !out_lo))) return fail(LGCN_E_ARG, "lgcn_sorted_segment_add: bad args");
+    if (B == 0) return LGCN_OK;
+    if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)))
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_sorted_segment_add: needs d %% 4 == 0 and aligned rows");
+    const auto* w = reinterpret_cast<const unsigned long long*>(sorted);
+    hipStream_t s = as_stream(stream);
+    switch (d) {
+        case 16: return launch_ssa<4, 1>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
+        case 32: return launch_ssa<8, 1>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
+        case 64: return launch_ssa<16, 1>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
+        case 128: return launch_ssa<32, 1>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
+        case 256: return launch_ssa<64, 1>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
+        case 512: return launch_ssa<64, 2>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
+        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_sorted_segment_add: d=%d", d);
+    }
+}
+
 int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* loss, lgcn_stream_t stream) {
     if (B < 0 || !loss || (B > 0 && !terms)) return fail(LGCN_E_ARG, "lgcn_bpr_loss: bad args");
-    k_bpr_loss<<<1, kBlock, 0, as_stream(stream)>>>(terms, B, d, coeff, loss);
+    k_bpr_loss<<<1, kLossBlock, 0, as_stream(stream)>>>(terms, B, d, coeff, loss);
     return check_launch("k_bpr_loss");
 }
 
 int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C, int64_t N, int32_t d,
-                      float* out_lo, float* out_hi, int64_t split, int32_t add, lgcn_stream_t stream) {
+                      float* out_lo, float* out_hi, int64_t split, int32_t add, float mul, float div,
+                      lgcn_stream_t stream) {
     if (N < 0 || d <= 0 || !rowptr || !out_lo || (split < N && !out_hi)) return fail(LGCN_E_ARG, "lgcn_segment_rows: bad args");
     if (N == 0) return LGCN_OK;
     if (d % 4 != 0 || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C && !al16(C)))
         return fail(LGCN_E_UNSUPPORTED, "lgcn_segment_rows: needs d %% 4 == 0 and aligned rows");
     hipStream_t s = as_stream(stream);
     switch (d) {
-        case 16: return launch_seg<4, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
-        case 32: return launch_seg<8, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
-        case 64: return launch_seg<16, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
-        case 128: return launch_seg<32, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
-        case 256: return launch_seg<64, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
-        case 512: return launch_seg<64, 2>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, s);
+        case 16: return launch_seg<4, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, mul, div, s);
+        case 32: return launch_seg<8, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, mul, div, s);
+        case 64: return launch_seg<16, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, mul, div, s);
+        case 128: return launch_seg<32, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, mul, div, s);
+        case 256: return launch_seg<64, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, mul, div, s);
+        case 512: return launch_seg<64, 2>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, mul, div, s);
         default: return fail(LGCN_E_UNSUPPORTED, "lgcn_segment_rows: d=%d (supported 16..512, powers of two)", d);
     }
 }

@@ -34,23 +34,25 @@ struct TensorList {
     int n;
 };
 
-__device__ __forceinline__ int tensor_of(const TensorList& t, int64_t i) {
-    int k = 0;
-#pragma unroll
-    for (int j = 1; j < kMaxTensors; ++j)
-        if (j < t.n && i >= t.offset[j]) k = j;
-    return k;
-}
-
 __global__ __launch_bounds__(kBlock) void k_sqnorm_partial(TensorList t, float* __restrict__ partial) {
     __shared__ float red[kBlock / 64];
     float acc = 0.f;
-    const int64_t total = t.offset[t.n];
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
-        const int k = tensor_of(t, i);
-        const float g = t.grad[k][i - t.offset[k]];
-        acc += g * g;
+    // per tensor: float4 sweep of the aligned body, scalar tail (fixed assignment -> deterministic)
+    for (int k = 0; k < t.n; ++k) {
+        const float* G = t.grad[k];
+        const int64_t n = t.numel[k];
+        int64_t done = 0;
+        if ((reinterpret_cast<uintptr_t>(G) & 15u) == 0) {
+            const int64_t n4 = n / 4;
+            const float4* G4 = reinterpret_cast<const float4*>(G);
+            for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
+                const float4 g = G4[i];
+                acc += g.x * g.x + g.y * g.y + g.z * g.z + g.w * g.w;
+            }
+            done = n4 * 4;
+        }
+        for (int64_t i = done + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) acc += G[i] * G[i];
     }
     // fixed-order wave + block reduction
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
@@ -100,9 +102,28 @@ __device__ __forceinline__ void adam_elem(float& p, float& g, float& m, float& v
     p = p + s.step_size * (m / denom);
 }
 
+// Device-side step counter and bias corrections (capturable Adam: a replayed hipGraph advances
+// the step on the device). Same double-precision formulas torch evaluates on the host.
+__global__ void k_adam_prologue(double* __restrict__ step, float lr, double beta1, double beta2,
+                                float* __restrict__ scalars) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        const double t = step[0] + 1.0;
+        step[0] = t;
+        const double bc1 = 1.0 - pow(beta1, t);
+        const double bc2 = 1.0 - pow(beta2, t);
+        scalars[0] = static_cast<float>(-(static_cast<double>(lr) / bc1));
+        scalars[1] = static_cast<float>(sqrt(bc2));
+    }
+}
+
 // One block-stride sweep per tensor, float4 where the tensor is 16-byte aligned and long enough.
-__global__ __launch_bounds__(kBlock) void k_adam(TensorList t, AdamScalars s, const float* __restrict__ clip) {
+__global__ __launch_bounds__(kBlock) void k_adam(TensorList t, AdamScalars s, const float* __restrict__ clip,
+                                                 const float* __restrict__ dev_scalars) {
     const float coef = clip ? clip[1] : 1.0f;
+    if (dev_scalars) {
+        s.step_size = dev_scalars[0];
+        s.bc2_sqrt = dev_scalars[1];
+    }
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int k = 0; k < t.n; ++k) {
         float* P = t.param[k];
@@ -184,16 +205,22 @@ int lgcn_grad_norm(const lgcn_adam_tensor_t* tensors, int32_t n, float max_norm,
     return check_launch("k_norm_finish");
 }
 
+int lgcn_adam_prologue(double* step, float lr, double beta1, double beta2, float* scalars, lgcn_stream_t stream) {
+    if (!step || !scalars) return fail(LGCN_E_ARG, "lgcn_adam_prologue: null pointer");
+    k_adam_prologue<<<1, 64, 0, as_stream(stream)>>>(step, lr, beta1, beta2, scalars);
+    return check_launch("k_adam_prologue");
+}
+
 int lgcn_adam_step(const lgcn_adam_tensor_t* tensors, int32_t n, float one_minus_beta1, float beta2,
                    float one_minus_beta2, float eps, float step_size, float bc2_sqrt, const float* clip,
-                   int32_t write_grad, lgcn_stream_t stream) {
+                   const float* dev_scalars, int32_t write_grad, lgcn_stream_t stream) {
     TensorList t;
     if (int rc = make_list(tensors, n, t, true)) return rc;
     AdamScalars sc{one_minus_beta1, beta2, one_minus_beta2, step_size, bc2_sqrt, eps, write_grad};
     const int64_t total = t.offset[t.n];
     if (total == 0) return LGCN_OK;
     const unsigned blocks = grid_for(total / 4 + 1, kBlock, 8192);
-    k_adam<<<blocks, kBlock, 0, as_stream(stream)>>>(t, sc, clip);
+    k_adam<<<blocks, kBlock, 0, as_stream(stream)>>>(t, sc, clip, dev_scalars);
     return check_launch("k_adam");
 }
 

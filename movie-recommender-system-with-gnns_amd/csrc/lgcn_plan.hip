@@ -92,12 +92,13 @@ __global__ void k_edge_norm(const int64_t* __restrict__ rowptr, const int32_t* _
 
 // ---- schedule ----
 __global__ void k_sched_count(const int64_t* __restrict__ rowptr, int64_t N, int32_t chunk,
-                              int64_t* __restrict__ n_items, int32_t* __restrict__ n_part,
-                              int32_t* __restrict__ n_split) {
+                              const uint8_t* __restrict__ row_mask, int64_t* __restrict__ n_items,
+                              int32_t* __restrict__ n_part, int32_t* __restrict__ n_split) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += stride) {
         const int64_t deg = rowptr[i + 1] - rowptr[i];
-        const int64_t nch = (deg > chunk) ? (deg + chunk - 1) / chunk : 1;
+        const bool live = (row_mask == nullptr) || row_mask[i];
+        const int64_t nch = !live ? 0 : (deg > chunk) ? (deg + chunk - 1) / chunk : 1;
         n_items[i] = nch;
         n_part[i] = (nch > 1) ? static_cast<int32_t>(nch) : 0;
         n_split[i] = (nch > 1) ? 1 : 0;
@@ -278,7 +279,7 @@ int lgcn_schedule_workspace_size(int64_t E, int64_t N, int32_t chunk, size_t* by
 }
 
 int lgcn_schedule_build(const int64_t* rowptr, int64_t N, int64_t E, int32_t chunk, int64_t side_split,
-                        lgcn_item_t* items, int64_t items_cap, lgcn_split_t* splits,
+                        const uint8_t* row_mask, lgcn_item_t* items, int64_t items_cap, lgcn_split_t* splits,
                         int64_t splits_cap, int64_t* counts, void* ws, size_t ws_bytes,
                         lgcn_stream_t stream) {
     if (!rowptr || !counts || N < 0 || E < 0 || chunk < 1 || chunk >= (1 << 30) || side_split < 0)
@@ -307,7 +308,7 @@ int lgcn_schedule_build(const int64_t* rowptr, int64_t N, int64_t E, int32_t chu
     if (!c.ok) return fail(LGCN_E_WORKSPACE, "lgcn_schedule_build: workspace %zu < %zu", ws_bytes, c.used);
 
     const unsigned g = grid_for(N, kBlock, 8192);
-    k_sched_count<<<g, kBlock, 0, s>>>(rowptr, N, chunk, n_items, n_part, n_split);
+    k_sched_count<<<g, kBlock, 0, s>>>(rowptr, N, chunk, row_mask, n_items, n_part, n_split);
     if (int rc = check_launch("k_sched_count")) return rc;
     size_t t = cub_bytes;
     if (int rc = check_hip(hipcub::DeviceScan::ExclusiveSum(cub_tmp, t, n_items, item_off, static_cast<int>(N), s), "scan items")) return rc;

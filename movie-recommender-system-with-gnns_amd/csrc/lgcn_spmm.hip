@@ -86,6 +86,11 @@ __device__ __forceinline__ void finish_row_vec(const SpmmArgs& a, int64_t r, int
     } else if (a.mode == LGCN_EPI_STORE) {
 #pragma unroll
         for (int k = 0; k < NV; ++k) acc[l + k * LPR] = v[k];
+    } else if (a.mode == LGCN_EPI_SCALE) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+            acc[l + k * LPR] = make_float4((v[k].x * a.mul) / a.div, (v[k].y * a.mul) / a.div,
+                                           (v[k].z * a.mul) / a.div, (v[k].w * a.mul) / a.div);
     } else {
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
@@ -224,6 +229,7 @@ __device__ __forceinline__ void finish_row_scalar(const SpmmArgs& a, int64_t r, 
         if (cidx < a.d) {
             float s;
             if (a.mode == LGCN_EPI_STORE) s = v[k];
+            else if (a.mode == LGCN_EPI_SCALE) s = (v[k] * a.mul) / a.div;
             else if (e) s = e[cidx] + v[k];
             else s = acc[cidx] + v[k];
             if (a.mode == LGCN_EPI_FINAL_ACC || a.mode == LGCN_EPI_FINAL_E) s = (s / a.div) * a.mul;
@@ -346,7 +352,7 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
               float div, float mul, lgcn_stream_t stream, int pass) {
     if (N < 0 || d <= 0 || n_items < 0 || n_splits < 0)
         return fail(LGCN_E_ARG, "lgcn_spmm: bad sizes (N=%lld d=%d)", (long long)N, d);
-    if (mode < LGCN_EPI_INIT || mode > LGCN_EPI_STORE) return fail(LGCN_E_ARG, "lgcn_spmm: bad mode %d", mode);
+    if (mode < LGCN_EPI_INIT || mode > LGCN_EPI_SCALE) return fail(LGCN_E_ARG, "lgcn_spmm: bad mode %d", mode);
     if (N == 0 || n_items == 0) return LGCN_OK;
     // col/val may be NULL for an edge-free plan (every item then has len 0)
     if (!items || !x_lo || !acc_lo) return fail(LGCN_E_ARG, "lgcn_spmm: null items/x/acc");

@@ -19,6 +19,7 @@ EPI_ADD = 1
 EPI_FINAL_ACC = 2
 EPI_FINAL_E = 3
 EPI_STORE = 4
+EPI_SCALE = 5
 
 ITEM_BYTES = 16   # lgcn_item_t {int64 beg; int32 len; int32 dst}
 SPLIT_BYTES = 16  # lgcn_split_t {int32 row, pbeg, pcnt, pad}
@@ -39,7 +40,7 @@ _SIGS = {
     "lgcn_inv_sqrt_degree": ([_vp, _i64, _vp, _vp], ctypes.c_int),
     "lgcn_edge_norm": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_schedule_workspace_size": ([_i64, _i64, _i32, ctypes.POINTER(_sz)], ctypes.c_int),
-    "lgcn_schedule_build": ([_vp, _i64, _i64, _i32, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _sz, _vp], ctypes.c_int),
+    "lgcn_schedule_build": ([_vp, _i64, _i64, _i32, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _sz, _vp], ctypes.c_int),
     "lgcn_spmm": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
                    _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp],
                   ctypes.c_int),
@@ -51,13 +52,20 @@ _SIGS = {
                           ctypes.c_int),
     "lgcn_scale": ([_vp, _vp, _i64, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_copy_scale": ([_vp, _vp, _i64, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),
-    "lgcn_bpr_fused": ([_vp, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _f32, _vp, _vp, _vp, _vp],
+    "lgcn_bpr_fused": ([_vp, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _f32, _f32, _f32, _vp, _vp,
+                        _vp, _vp],
                        ctypes.c_int),
     "lgcn_bpr_loss": ([_vp, _i64, _i32, _f32, _vp, _vp], ctypes.c_int),
-    "lgcn_segment_rows": ([_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _i32, _vp], ctypes.c_int),
+    "lgcn_segment_rows": ([_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _i32, _f32, _f32, _vp], ctypes.c_int),
+    "lgcn_sort_keys_small": ([_vp, _i64, _i64, _vp, _vp], ctypes.c_int),
+    "lgcn_range_scatter_add": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp],
+                               ctypes.c_int),
+    "lgcn_flagged_rows_add": ([_vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _i64, _vp], ctypes.c_int),
+    "lgcn_sorted_segment_add": ([_vp, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_grad_norm_workspace_floats": ([], ctypes.c_int),
     "lgcn_grad_norm": ([_vp, _i32, _f32, _vp, _vp, _vp], ctypes.c_int),
-    "lgcn_adam_step": ([_vp, _i32, _f32, _f32, _f32, _f32, _f32, _f32, _vp, _i32, _vp], ctypes.c_int),
+    "lgcn_adam_step": ([_vp, _i32, _f32, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _i32, _vp], ctypes.c_int),
+    "lgcn_adam_prologue": ([_vp, _f32, ctypes.c_double, ctypes.c_double, _vp, _vp], ctypes.c_int),
     "lgcn_partition_edges": ([_vp, _vp, _i64, _i64, _i32, _i32, _f32, _vp], ctypes.c_int),
     "lgcn_partition_last_error": ([], ctypes.c_char_p),
 }

@@ -17,14 +17,18 @@ from . import _ffi
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 max_grad_norm: float | None = None, keep_clipped_grad: bool = True):
+                 max_grad_norm: float | None = None, keep_clipped_grad: bool = True, capturable: bool = False):
+        """capturable=True keeps the step counter and bias corrections on the device
+        (lgcn_adam_prologue), so the step can be captured in a hipGraph and replayed."""
         if not 0.0 <= lr:
             raise ValueError(f"Invalid learning rate: {lr}")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
         self.fused_clip_norm = max_grad_norm
         self.keep_clipped_grad = keep_clipped_grad
+        self.capturable = capturable
         self.last_norm = None  # device tensor [total_norm, clip_coef] of the last clipped step
         self._norm_ws = None
+        self._norm_out = None
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -47,11 +51,14 @@ class FusedAdam(torch.optim.Optimizer):
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
+            if self.capturable and "dev_step" not in group:
+                group["dev_step"] = torch.zeros(1, dtype=torch.float64, device=ps[0].device)
+                group["dev_scalars"] = torch.zeros(2, dtype=torch.float32, device=ps[0].device)
             for i in range(0, len(ps), 8):
-                self._step_chunk(lib, group, ps[i:i + 8])
+                self._step_chunk(lib, group, ps[i:i + 8], first=(i == 0))
         return loss
 
-    def _step_chunk(self, lib, group, ps):
+    def _step_chunk(self, lib, group, ps, first=True):
         dev = ps[0].device
         stream = _ffi.stream_of(dev)
         arr = (_ffi.AdamTensor * len(ps))()
@@ -63,20 +70,29 @@ class FusedAdam(torch.optim.Optimizer):
         if self.fused_clip_norm is not None:
             if self._norm_ws is None or self._norm_ws.device != dev:
                 self._norm_ws = torch.empty(lib.lgcn_grad_norm_workspace_floats(), dtype=torch.float32, device=dev)
-            out = torch.empty(2, dtype=torch.float32, device=dev)
+                self._norm_out = torch.empty(2, dtype=torch.float32, device=dev)
+            out = self._norm_out
             _ffi.check(lib.lgcn_grad_norm(arr, len(ps), float(self.fused_clip_norm), self._norm_ws.data_ptr(),
                                           out.data_ptr(), stream), "lgcn_grad_norm")
             self.last_norm = out
-            clip_ptr = out.data_ptr() + 0  # kernel reads element [1]
+            clip_ptr = out.data_ptr()  # kernel reads element [1]
         beta1, beta2 = group["betas"]
         st0 = self.state[ps[0]]
         # every param of a group advances together (as the reference's single-group Adam)
         step = st0["step"] + 1
         for p in ps:
             self.state[p]["step"] = step
-        bc1 = 1 - beta1 ** step
-        bc2 = 1 - beta2 ** step
-        step_size = -(group["lr"] / bc1)
+        dev_scalars = None
+        if self.capturable:
+            if first:  # one device step per group
+                _ffi.check(lib.lgcn_adam_prologue(group["dev_step"].data_ptr(), group["lr"], beta1, beta2,
+                                                  group["dev_scalars"].data_ptr(), stream), "lgcn_adam_prologue")
+            dev_scalars = ctypes.c_void_p(group["dev_scalars"].data_ptr())
+            step_size, bc2_sqrt = 0.0, 1.0
+        else:
+            bc1 = 1 - beta1 ** step
+            bc2 = 1 - beta2 ** step
+            step_size, bc2_sqrt = -(group["lr"] / bc1), bc2 ** 0.5
         _ffi.check(lib.lgcn_adam_step(arr, len(ps), 1 - beta1, beta2, 1 - beta2, group["eps"], step_size,
-                                      bc2 ** 0.5, ctypes.c_void_p(clip_ptr) if clip_ptr else None,
+                                      bc2_sqrt, ctypes.c_void_p(clip_ptr) if clip_ptr else None, dev_scalars,
                                       1 if self.keep_clipped_grad else 0, stream), "lgcn_adam_step")

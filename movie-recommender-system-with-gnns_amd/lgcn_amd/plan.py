@@ -44,8 +44,57 @@ class CsrDirection:
         return torch.stack([it[:, 0], lens_dst[:, 0].long(), lens_dst[:, 1].long()], dim=1)
 
 
+def _schedule(rowptr: torch.Tensor, N: int, E: int, chunk: int, side_split: int, row_mask, stream: int):
+    lib = _ffi.load()
+    dev = rowptr.device
+    bytes_ = _ffi._sz(0)
+    _ffi.check(lib.lgcn_schedule_workspace_size(E, N, chunk, bytes_), "lgcn_schedule_workspace_size")
+    ws2 = torch.empty(max(1, bytes_.value), dtype=torch.uint8, device=dev)
+    cap = N + E // chunk + 1
+    items = torch.empty((cap, 2), dtype=torch.int64, device=dev)
+    splits = torch.empty((max(N, 1), 4), dtype=torch.int32, device=dev)
+    counts = torch.zeros(3, dtype=torch.int64, device=dev)
+    _ffi.check(lib.lgcn_schedule_build(rowptr.data_ptr(), N, E, chunk, side_split, _ffi.ptr(row_mask), items.data_ptr(),
+                                       cap, splits.data_ptr(), splits.shape[0], counts.data_ptr(), ws2.data_ptr(),
+                                       ws2.numel(), stream), "lgcn_schedule_build")
+    n_items, n_splits, n_partials = (int(v) for v in counts.cpu().tolist())
+    return items, splits, n_items, n_splits, n_partials
+
+
+def segment_directions(keys: torch.Tensor, N: int, chunk: int = DEFAULT_CHUNK):
+    """Plans for summing rows C[j] into output row keys[j] (j = 0..M-1) with lgcn_spmm, weight 1,
+    in j order within a row: (dense: every row scheduled, for a SCALE/STORE pass that also writes
+    the empty rows; sparse: only rows with a contribution, for an ADD pass). Built once per
+    Cluster-GCN batch for its fixed (user, positive) gradient rows."""
+    lib = _ffi.load()
+    dev = keys.device
+    M = keys.numel()
+    stream = _ffi.stream_of(dev)
+    # lgcn_csr_build range-checks `other` (= the contribution index) against its node count too,
+    # so build over max(N, M) rows; rows >= N stay empty and are sliced off
+    Nb = max(N, M)
+    bytes_ = _ffi._sz(0)
+    _ffi.check(lib.lgcn_csr_workspace_size(M, Nb, bytes_), "lgcn_csr_workspace_size")
+    ws = torch.empty(max(1, bytes_.value), dtype=torch.uint8, device=dev)
+    rowptr_b = torch.empty(Nb + 1, dtype=torch.int64, device=dev)
+    col = torch.empty(M, dtype=torch.int32, device=dev)
+    eid = torch.empty(M, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int64, device=dev)
+    other = torch.arange(M, dtype=torch.int64, device=dev)
+    _ffi.check(lib.lgcn_csr_build(keys.data_ptr(), other.data_ptr(), M, Nb, rowptr_b.data_ptr(), col.data_ptr(),
+                                  eid.data_ptr(), err.data_ptr(), ws.data_ptr(), ws.numel(), stream), "lgcn_csr_build")
+    rowptr = rowptr_b[: N + 1].contiguous()
+    val = torch.ones(M, dtype=torch.float32, device=dev)
+    mask = (rowptr[1:] > rowptr[:-1]).to(torch.uint8)
+    dense = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, None, stream), chunk)
+    sparse = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, mask, stream), chunk)
+    if int(err.item()):
+        raise IndexError("segment keys out of range")
+    return dense, sparse
+
+
 def _build_direction(key: torch.Tensor, other: torch.Tensor, N: int, chunk: int, side_split: int,
-                     dis: torch.Tensor | None, stream: int) -> tuple[CsrDirection, torch.Tensor, int]:
+                     dis: torch.Tensor | None, stream: int, row_mask: torch.Tensor | None = None) -> tuple[CsrDirection, torch.Tensor, int]:
     lib = _ffi.load()
     dev = key.device
     E = key.numel()
@@ -72,7 +121,7 @@ def _build_direction(key: torch.Tensor, other: torch.Tensor, N: int, chunk: int,
     items = torch.empty((cap, 2), dtype=torch.int64, device=dev)
     splits = torch.empty((max(N, 1), 4), dtype=torch.int32, device=dev)
     counts = torch.zeros(3, dtype=torch.int64, device=dev)
-    _ffi.check(lib.lgcn_schedule_build(rowptr.data_ptr(), N, E, chunk, side_split, items.data_ptr(), cap, splits.data_ptr(),
+    _ffi.check(lib.lgcn_schedule_build(rowptr.data_ptr(), N, E, chunk, side_split, _ffi.ptr(row_mask), items.data_ptr(), cap, splits.data_ptr(),
                                        splits.shape[0], counts.data_ptr(), ws2.data_ptr(), ws2.numel(), stream),
                "lgcn_schedule_build")
     # one host read-back per plan: ids check + schedule sizes (the launches need them)
@@ -85,7 +134,11 @@ def _build_direction(key: torch.Tensor, other: torch.Tensor, N: int, chunk: int,
 class PropagationPlan:
     """Forward (+ lazily transposed) plan for one edge set over N = num_users + num_items nodes."""
 
-    def __init__(self, edge_index: torch.Tensor, num_nodes: int, chunk: int = DEFAULT_CHUNK, side_split: int = 0):
+    def __init__(self, edge_index: torch.Tensor, num_nodes: int, chunk: int = DEFAULT_CHUNK, side_split: int = 0,
+                 touched_only: bool = False):
+        """touched_only: schedule only rows incident to an edge of this edge set (both directions);
+        rows outside are never written by a propagation over this plan. ``touched`` (uint8[N])
+        marks them. Used by the sparse Cluster-GCN batch step (lgcn_amd.train_step)."""
         _ffi.require_device(edge_index, "PropagationPlan")
         if edge_index.dim() != 2 or edge_index.shape[0] != 2:
             raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
@@ -99,9 +152,18 @@ class PropagationPlan:
         self._src = edge_index[0].contiguous()
         self._dst = edge_index[1].contiguous()
         stream = _ffi.stream_of(self.device)
+        self.touched = None
+        if touched_only:
+            t = torch.zeros(self.num_nodes, dtype=torch.uint8, device=self.device)
+            if self.num_edges:
+                if int(edge_index.min()) < 0 or int(edge_index.max()) >= self.num_nodes:
+                    raise IndexError(f"edge_index holds node ids outside [0, {self.num_nodes})")
+                t[self._src] = 1
+                t[self._dst] = 1
+            self.touched = t
         # forward: rows = targets (PyG flow source_to_target aggregates at edge_index[1])
         self.fwd, self.dis, bad = _build_direction(self._dst, self._src, self.num_nodes, self.chunk,
-                                                 self.side_split, None, stream)
+                                                 self.side_split, None, stream, self.touched)
         if bad:
             raise IndexError(f"edge_index holds {bad} edge(s) with a node id outside [0, {self.num_nodes})")
         self._bwd: CsrDirection | None = None
@@ -113,7 +175,7 @@ class PropagationPlan:
         if self._bwd is None:
             stream = _ffi.stream_of(self.device)
             self._bwd, _, _ = _build_direction(self._src, self._dst, self.num_nodes, self.chunk,
-                                              self.side_split, self.dis, stream)
+                                              self.side_split, self.dis, stream, self.touched)
         return self._bwd
 
     def nbytes(self) -> int:

@@ -146,6 +146,35 @@ def propagate_backward(dout: torch.Tensor, plan: PropagationPlan, U: int, K: int
     return grad_user, grad_item
 
 
+def propagate_backward_seeded(grad_user: torch.Tensor, grad_item: torch.Tensor, plan: PropagationPlan, K: int) -> None:
+    """In-place backward for the sparse batch step: on entry the two gradient tables hold the seed
+    g = (dF * mul) / div for EVERY row; on exit they hold dL/dx0. Only the plan's scheduled rows
+    change (with a touched-only plan, rows no batch edge reaches keep g, which is their exact
+    gradient: every layer adds 0 to them)."""
+    U, d = grad_user.shape
+    I = grad_item.shape[0]
+    N = U + I
+    if K == 0:
+        return
+    dev = grad_user.device
+    stream = _ffi.stream_of(dev)
+    b = plan.bwd
+    partial = torch.empty((b.n_partials, d), dtype=torch.float32, device=dev) if b.n_partials else None
+    g = (grad_user, grad_item, U)
+    if K == 1:
+        # the gather source must not alias the table being written
+        src = torch.cat([grad_user, grad_item])
+        spmm(b, N, d, (src, None, N), g, g, None, _ffi.EPI_INIT, 1.0, 1.0, partial, stream)
+        return
+    bufs = [torch.empty((N, d), dtype=torch.float32, device=dev) for _ in range(min(2, K - 1))]
+    cur = g
+    for step in range(K):
+        last = step == K - 1
+        acc = g if last else (bufs[step % len(bufs)], None, N)
+        spmm(b, N, d, cur, g, acc, None, _ffi.EPI_INIT, 1.0, 1.0, partial, stream)
+        cur = acc
+
+
 class LightGCNPropagation(torch.autograd.Function):
     """autograd node for the whole K-layer propagation (one node instead of K LGConv nodes)."""
 

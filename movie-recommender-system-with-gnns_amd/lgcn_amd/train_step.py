@@ -2,13 +2,20 @@
 (reference utils/train_test.py:86-101: zero_grad, compute_embeddings, bpr_loss, backward,
 clip_grad_norm_(1), Adam step) as a fixed sequence of HIP launches.
 
-    out  = LightGCN forward over the batch edges       (lgcn_spmm x K, cached plan)
+    out  = LightGCN forward over the batch edges       (lgcn_spmm x K over a touched-only plan)
     neg  = torch.randint(0, I, (B,))                   (same draw as reference sample_negative)
     loss, per-triplet grad rows = lgcn_bpr_fused       (+ lgcn_bpr_loss)
-    dF   = rows scattered in a fixed order             (lgcn_csr_build over the 3B keys + lgcn_segment_rows)
-    grads = LightGCN backward of dF                    (lgcn_scale + lgcn_spmm x K, transposed plan)
+    g    = scaled dF rows in a fixed order, written    (lgcn_csr_build over the 3B keys +
+           straight into the two gradient tables        lgcn_segment_rows with the backward scale)
+    grads = LightGCN backward seeded with g, in place (lgcn_spmm x K, transposed touched-only plan)
           + reg-gradient rows                          (lgcn_segment_rows, add)
     [all_reduce grads over ranks]; FusedAdam (clip fused) or any torch optimizer
+
+Sparse batch (exact): a Cluster-GCN batch's edges touch a few % of the N rows. Its plans schedule
+only those rows. A row no batch edge reaches gets an exact 0 from every layer, so its final
+embedding is (x0 / (K+1)) * fp32(1/(K+1)) — lgcn_bpr_fused computes that on the fly for
+negatives that land there — and its gradient is just the seed g. So no full-N epilogue runs;
+the only dense passes left are the gradient-table write and the optimizer.
 
 Per batch the (user, positive) triplet halves are a fixed function of the batch edges
 (reference utils/helpers.py:98-99), so they are computed once and cached with the plan; only the
@@ -21,7 +28,9 @@ import weakref
 import torch
 
 from . import _ffi
-from .propagate import propagate_backward, propagate_forward
+import numpy as np
+
+from .propagate import propagate_backward_seeded, propagate_forward, spmm
 
 
 class _BatchState:
@@ -29,7 +38,10 @@ class _BatchState:
         dev = edge_index.device
         U, I = model.num_users, model.num_items
         N = U + I
-        self.plan = model.plan_for(edge_index)
+        from .plan import PropagationPlan
+
+        # short chunks: a batch has few edges, so latency (not bandwidth) bounds its item passes
+        self.plan = PropagationPlan(edge_index, N, 32, side_split=U, touched_only=True)
         src, dst = edge_index[0], edge_index[1]
         self.users = src[src < U].contiguous()
         self.pos = (dst[dst >= U] - U).contiguous()
@@ -40,6 +52,15 @@ class _BatchState:
         self.keys = torch.empty(3 * B, dtype=torch.int64, device=dev)
         self.keys[:B] = self.users
         self.keys[B:2 * B] = self.pos + U
+        # fixed (user, positive) gradient rows: load-balanced segment plans, built once per batch
+        from .plan import segment_directions
+
+        self.small = 2 * B <= N  # segment plans index contributions as node ids (always true for real batches)
+        if self.small:
+            self.fixed_dense, self.fixed_sparse = segment_directions(self.keys[:2 * B], N, chunk=32)
+            self.c2buf = torch.empty((B, d), dtype=torch.float32, device=dev)
+            self.c2flag = torch.empty(B, dtype=torch.uint8, device=dev)
+            self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         self.cf = torch.empty((3 * B, d), dtype=torch.float32, device=dev)
         self.cw = torch.empty((3 * B, d), dtype=torch.float32, device=dev)
         self.terms = torch.empty(2 * B, dtype=torch.float32, device=dev)
@@ -61,12 +82,20 @@ class FusedTrainStep:
     step(batch) -> device loss tensor [1]: gradients, optional DP all-reduce, optimizer step.
     compute_grads(batch) -> loss: sets user/item_embedding.weight.grad only."""
 
-    def __init__(self, model, optimizer, bpr_coeff: float = 5e-3, world: int = 1, max_entries: int = 4096):
+    def __init__(self, model, optimizer, bpr_coeff: float = 5e-3, world: int = 1, max_entries: int = 4096,
+                 graphs: bool = False):
+        """graphs=True: the first step of each batch runs eagerly, then the whole step (gradients
+        and, at world == 1, the optimizer — which must be a capturable FusedAdam) is captured in a
+        per-batch hipGraph and replayed from then on; negatives still come from the global CUDA
+        generator (graph-safe Philox offsets), so each replay draws new ones."""
         self.model = model
         self.optimizer = optimizer
         self.coeff = float(bpr_coeff)
         self.world = world
         self.max_entries = max_entries
+        self.graphs = graphs
+        if graphs and world == 1 and not getattr(optimizer, "capturable", False):
+            raise ValueError("graphs=True needs a capturable optimizer (lgcn_amd.optim.FusedAdam(capturable=True))")
         self._states: dict[int, tuple[weakref.ref, int, _BatchState]] = {}
 
     def state(self, edge_index: torch.Tensor) -> _BatchState:
@@ -93,36 +122,99 @@ class FusedTrainStep:
         B = st.B
         dev = uw.device
         stream = _ffi.stream_of(dev)
+        div = float(K + 1)
+        mul = float(np.float32(1.0 / (K + 1)))
         with torch.no_grad():
             out = propagate_forward(uw.detach(), iw.detach(), st.plan, K)
             torch.randint(0, I, (B,), device=dev, out=st.neg)
             torch.add(st.neg, U, out=st.keys[2 * B:])
             _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
                                           st.users.data_ptr(), st.pos.data_ptr(), st.neg.data_ptr(), B, d,
+                                          st.plan.touched.data_ptr(), div, mul,
                                           self.coeff, st.cf.data_ptr(), st.cw.data_ptr(), st.terms.data_ptr(),
                                           stream), "lgcn_bpr_fused")
             _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(), stream),
                        "lgcn_bpr_loss")
-            _ffi.check(lib.lgcn_csr_build(st.keys.data_ptr(), st.keys.data_ptr(), 3 * B, N, st.rowptr.data_ptr(),
-                                          st.col.data_ptr(), st.eid.data_ptr(), st.err.data_ptr(), st.ws.data_ptr(),
-                                          st.ws.numel(), stream), "lgcn_csr_build")
-            dF = torch.empty((N, d), dtype=torch.float32, device=dev)
-            _ffi.check(lib.lgcn_segment_rows(st.rowptr.data_ptr(), st.eid.data_ptr(), st.cf.data_ptr(), N, d,
-                                             dF.data_ptr(), None, N, 0, stream), "lgcn_segment_rows")
-            gu, gi = propagate_backward(dF, st.plan, U, K)
-            _ffi.check(lib.lgcn_segment_rows(st.rowptr.data_ptr(), st.eid.data_ptr(), st.cw.data_ptr(), N, d,
-                                             gu.data_ptr(), gi.data_ptr(), U, 1, stream), "lgcn_segment_rows")
+            gu = torch.empty((U, d), dtype=torch.float32, device=dev)
+            gi = torch.empty((I, d), dtype=torch.float32, device=dev)
+            grads = (gu, gi, U)
+            if st.small:
+                # g = (dF * mul) / div: fixed rows through the per-batch plan (every row written, 0 if
+                # empty), then the negatives' rows sorted in one workgroup and added run by run
+                big = 1 << 62
+                spmm(st.fixed_dense, N, d, (st.cf, None, big), None, grads, None, _ffi.EPI_SCALE, div, mul,
+                     stream=stream)
+                # negatives: dF rows into g now, their reg rows parked (per row, first-occurrence slot)
+                _ffi.check(lib.lgcn_range_scatter_add(st.neg.data_ptr(), B, I, U, st.cf[2 * B:].data_ptr(), d,
+                                                      gu.data_ptr(), gi.data_ptr(), U, mul, div,
+                                                      st.cw[2 * B:].data_ptr(), st.c2buf.data_ptr(),
+                                                      st.c2flag.data_ptr(), st.overflow.data_ptr(), stream),
+                           "lgcn_range_scatter_add")
+                propagate_backward_seeded(gu, gi, st.plan, K)
+                spmm(st.fixed_sparse, N, d, (st.cw, None, big), None, grads, None, _ffi.EPI_ADD, stream=stream)
+                _ffi.check(lib.lgcn_flagged_rows_add(st.neg.data_ptr(), B, U, st.c2buf.data_ptr(),
+                                                     st.c2flag.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U,
+                                                     stream), "lgcn_flagged_rows_add")
+            else:
+                # large batches: one stable radix sort of all 3B row keys per step
+                _ffi.check(lib.lgcn_csr_build(st.keys.data_ptr(), st.keys.data_ptr(), 3 * B, N, st.rowptr.data_ptr(),
+                                              st.col.data_ptr(), st.eid.data_ptr(), st.err.data_ptr(),
+                                              st.ws.data_ptr(), st.ws.numel(), stream), "lgcn_csr_build")
+                _ffi.check(lib.lgcn_segment_rows(st.rowptr.data_ptr(), st.eid.data_ptr(), st.cf.data_ptr(), N, d,
+                                                 gu.data_ptr(), gi.data_ptr(), U, 0, mul, div, stream),
+                           "lgcn_segment_rows")
+                propagate_backward_seeded(gu, gi, st.plan, K)
+                _ffi.check(lib.lgcn_segment_rows(st.rowptr.data_ptr(), st.eid.data_ptr(), st.cw.data_ptr(), N, d,
+                                                 gu.data_ptr(), gi.data_ptr(), U, 1, 1.0, 1.0, stream),
+                           "lgcn_segment_rows")
         uw.grad = gu
         iw.grad = gi
         return st.loss
 
-    def step(self, batch) -> torch.Tensor:
-        loss = self.compute_grads(batch)
-        if self.world > 1:
-            from .distributed import allreduce_grads
+    def check_overflow(self) -> None:
+        """Raise if any step's negative scatter overflowed a workgroup list (never expected for
+        uniform negatives; one host read per batch state — call once per epoch)."""
+        for ref, _, st in self._states.values():
+            if getattr(st, "overflow", None) is not None and int(st.overflow.item()):
+                raise RuntimeError("lgcn_range_scatter_add overflowed: negatives too concentrated for its lists")
 
-            allreduce_grads([self.model.user_embedding.weight, self.model.item_embedding.weight], self.world)
+    def _optimize(self) -> None:
         if getattr(self.optimizer, "fused_clip_norm", None) is None:
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=1)
         self.optimizer.step()
-        return loss
+
+    def _allreduce(self) -> None:
+        from .distributed import allreduce_grads
+
+        allreduce_grads([self.model.user_embedding.weight, self.model.item_embedding.weight], self.world)
+
+    def step(self, batch) -> torch.Tensor:
+        if not self.graphs:
+            loss = self.compute_grads(batch)
+            if self.world > 1:
+                self._allreduce()
+            self._optimize()
+            return loss
+        st = self.state(batch.edge_index)
+        if getattr(st, "graph", None) is None:
+            # real first step (warms every allocation and the optimizer state), then capture
+            loss = self.compute_grads(batch)
+            if self.world > 1:
+                self._allreduce()
+            self._optimize()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                st.graph_loss = self.compute_grads(batch)
+                st.graph_grads = (self.model.user_embedding.weight.grad, self.model.item_embedding.weight.grad)
+                if self.world == 1:
+                    self._optimize()
+            st.graph = g
+            return loss
+        st.graph.replay()
+        m = self.model
+        m.user_embedding.weight.grad, m.item_embedding.weight.grad = st.graph_grads
+        if self.world > 1:
+            self._allreduce()
+            self._optimize()
+        return st.graph_loss

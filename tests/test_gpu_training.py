@@ -134,10 +134,13 @@ def test_fused_adam_matches_torch(gpu):
             assert (x - y).abs().max().item() <= 1e-6 * max(1.0, x.abs().max().item()) + 1e-8
 
 
-@pytest.mark.parametrize("K,d", [(3, 64), (2, 128), (1, 32)])
-def test_fused_train_step_matches_autograd(gpu, K, d):
-    """lgcn_amd.train_step (no autograd: fused BPR kernel + sorted scatter + HIP backward) ==
-    the reference harness on the HIP model with autograd, same negatives (same CUDA seed)."""
+@pytest.mark.parametrize("K,d,cluster", [(3, 64, False), (2, 128, False), (1, 32, False), (3, 64, True),
+                                         (1, 64, True), (4, 128, True)])
+def test_fused_train_step_matches_autograd(gpu, K, d, cluster):
+    """lgcn_amd.train_step (no autograd: fused BPR kernel + sorted scatter + sparse HIP backward) ==
+    the reference harness on the HIP model with autograd, same negatives (same CUDA seed).
+    cluster=True: the batch is one Cluster-GCN part of 8, so most rows (and most negatives) are
+    untouched by the batch edges — the sparse-plan paths."""
     from lgcn_amd.train_step import FusedTrainStep
     from models.light_gcn import LightGCN
     from utils import train_test as TT
@@ -145,6 +148,12 @@ def test_fused_train_step_matches_autograd(gpu, K, d):
     import graphs
 
     U, I, ei = graphs.subsampled(U=400, I=250, pairs=5000, seed=K)
+    if cluster:
+        from lgcn_amd import cluster as C
+
+        part = C.partition_nodes(ei, U + I, 8)
+        ei = C.intra_part_edges(ei, part, 8)[3]
+        assert 0 < ei.shape[1] < 0.3 * 5000
     torch.manual_seed(1)
     a = LightGCN(U, I, num_layers=K, dim_h=d).to(gpu)
     b = LightGCN(U, I, num_layers=K, dim_h=d).to(gpu)
@@ -179,3 +188,31 @@ def test_fused_train_step_deterministic(gpu):
         step.compute_grads(batch)
         res.append((m.user_embedding.weight.grad.clone(), m.item_embedding.weight.grad.clone()))
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+def test_graph_replay_equals_eager(gpu):
+    """A hipGraph-replayed fused step (capturable FusedAdam) == the eager fused step, bitwise,
+    given the same CUDA seed before each step."""
+    from lgcn_amd import cluster as C
+    from lgcn_amd.optim import FusedAdam
+    from lgcn_amd.train_step import FusedTrainStep
+    from models.light_gcn import LightGCN
+
+    import graphs
+
+    U, I, ei = graphs.subsampled(U=500, I=300, pairs=6000, seed=4)
+    part = C.partition_nodes(ei, U + I, 4)
+    batches = [_Batch(torch.from_numpy(x).to(gpu)) for x in C.intra_part_edges(ei, part, 4)]
+    res = []
+    for use_graphs in (False, True):
+        torch.manual_seed(0)
+        m = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
+        opt = FusedAdam(m.parameters(), lr=1e-2, max_grad_norm=1, capturable=True)
+        step = FusedTrainStep(m, opt, graphs=use_graphs)
+        losses = []
+        for i in range(12):
+            torch.cuda.manual_seed(100 + i)
+            losses.append(step.step(batches[i % 4]).item())
+        res.append((losses, m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
