@@ -381,6 +381,8 @@ def run_train(args):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if fused is not None:
+        fused.check_overflow()  # outside the timed region: one host read per batch state
     if world > 1:
         t = torch.tensor([elapsed, edges], dtype=torch.float64, device=dev)
         tt = t.clone()

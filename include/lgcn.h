@@ -210,14 +210,10 @@ int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* 
 int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C, int64_t N, int32_t d,
                       float* out_lo, float* out_hi, int64_t split, int32_t add, float mul, float div,
                       lgcn_stream_t stream);
-/* The per-step part of that scatter for the B random negatives, without a general sort:
- *   lgcn_sort_keys_small: one workgroup sorts (keys[b] + key_offset, b) pairs (B <= 16384) into
- *     sorted[] (uint64 = row << 32 | b);
- *   lgcn_sorted_segment_add: out[row] += (sum of C[b] over the run of equal rows, in b order)
- *     * mul / div. (The users/positives part has a fixed structure per batch and goes through a
- *     load-balanced plan built once, with lgcn_spmm SCALE / ADD epilogues.) */
-int lgcn_sort_keys_small(const int64_t* keys, int64_t B, int64_t key_offset, uint64_t* sorted, lgcn_stream_t stream);
-/* Same result as sort + sorted_segment_add in ONE launch: out[key_offset + keys[b]] += (sum over b,
+/* The per-step part of that scatter for the B random negatives, in ONE launch and without a
+ * sort (the users/positives part has a fixed structure per batch and goes through a
+ * load-balanced plan built once, with lgcn_spmm SCALE / ADD epilogues):
+ * out[key_offset + keys[b]] += (sum over b,
  * in b order, of C[b]) * mul / div for keys in [0, nrows). Workgroup w owns a key range and keeps
  * its keys in b order by an ordered block compaction; used for the per-step negatives.
  * Optional second source C2 (nullable): the same per-row sums of C2 are parked in c2buf[b_first]
@@ -230,8 +226,6 @@ int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_
 int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, const float* c2buf,
                           const uint8_t* c2flag, int32_t d, float* out_lo, float* out_hi, int64_t split,
                           lgcn_stream_t stream);
-int lgcn_sorted_segment_add(const uint64_t* sorted, int64_t B, const float* C, int32_t d, float* out_lo,
-                            float* out_hi, int64_t split, float mul, float div, lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Training-step tail (reference utils/train_test.py:95-96: clip_grad_norm_(max_norm=1) then

@@ -220,75 +220,6 @@ __global__ __launch_bounds__(kBlock) void k_segment_rows(const int64_t* __restri
 }
 
 // ---- per-step scatter of the negatives' gradient rows (deterministic, no atomics) ----
-constexpr int kSmallSort = 16384;
-
-// One workgroup bitonic-sorts B <= 16384 packed (row << 32 | index) words in LDS; equal rows
-// keep index order (the index is the low word), so each row's contributions come out in a fixed
-// order whatever the scheduling.
-__global__ __launch_bounds__(1024) void k_sort_small(const int64_t* __restrict__ keys, int64_t B, int64_t key_offset,
-                                                     unsigned long long* __restrict__ out) {
-    __shared__ unsigned long long sh[kSmallSort];
-    int P = 1;
-    while (P < B) P <<= 1;
-    for (int i = threadIdx.x; i < P; i += blockDim.x)
-        sh[i] = (i < B) ? ((static_cast<unsigned long long>(keys[i] + key_offset) << 32) | static_cast<unsigned>(i))
-                        : ~0ull;
-    __syncthreads();
-    for (int k = 2; k <= P; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < P; i += blockDim.x) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const unsigned long long a = sh[i], b = sh[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) {
-                        sh[i] = b;
-                        sh[ixj] = a;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (int i = threadIdx.x; i < B; i += blockDim.x) out[i] = sh[i];
-}
-
-// One lane group per sorted position; the head of each run of equal rows sums the run's C rows
-// in index order and adds (sum * mul) / div into its output row.
-template <int LPR, int NV>
-__global__ __launch_bounds__(kBlock) void k_sorted_segment_add(const unsigned long long* __restrict__ sorted, int64_t B,
-                                                               const float* __restrict__ C, int32_t d, float* out_lo,
-                                                               float* out_hi, int64_t split, float mul, float div) {
-    constexpr int GPB = kBlock / LPR;
-    const int g = threadIdx.x / LPR;
-    const int l = threadIdx.x % LPR;
-    const int64_t j = int64_t(blockIdx.x) * GPB + g;
-    if (j >= B) return;
-    const unsigned long long w = sorted[j];
-    const int64_t row = static_cast<int64_t>(w >> 32);
-    if (j > 0 && static_cast<int64_t>(sorted[j - 1] >> 32) == row) return;
-    float4 acc[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t e = j; e < B; ++e) {
-        const unsigned long long we = sorted[e];
-        if (static_cast<int64_t>(we >> 32) != row) break;
-        const float4* c = reinterpret_cast<const float4*>(C + int64_t(static_cast<unsigned>(we)) * d) + l;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-            const float4 v = c[k * LPR];
-            acc[k] = make_float4(acc[k].x + v.x, acc[k].y + v.y, acc[k].z + v.z, acc[k].w + v.w);
-        }
-    }
-    float4* o = reinterpret_cast<float4*>(srow(out_lo, out_hi, split, row, int64_t(d))) + l;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        const float4 v = o[k * LPR];
-        o[k * LPR] = make_float4(v.x + (acc[k].x * mul) / div, v.y + (acc[k].y * mul) / div,
-                                 v.z + (acc[k].z * mul) / div, v.w + (acc[k].w * mul) / div);
-    }
-}
-
 // Range-owner scatter: workgroup w owns output rows [key_offset + w*span, ... + span). It streams
 // all B keys in index order, keeps the ones in its range through an ORDERED block compaction
 // (wave ballot + per-wave prefix), so its list is in b order, then every first occurrence of a row
@@ -476,17 +407,6 @@ int launch_fra(const int64_t* keys, int64_t B, int64_t key_offset, const float* 
 }
 
 template <int LPR, int NV>
-int launch_ssa(const unsigned long long* sorted, int64_t B, const float* C, int32_t d, float* lo, float* hi,
-               int64_t split, float mul, float div, hipStream_t s) {
-    constexpr int GPB = kBlock / LPR;
-    const int64_t blocks = (B + GPB - 1) / GPB;
-    if (blocks > 0)
-        k_sorted_segment_add<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(sorted, B, C, d, lo, hi,
-                                                                                           split, mul, div);
-    return check_launch("k_sorted_segment_add");
-}
-
-template <int LPR, int NV>
 int launch_bpr(const BprArgs& a, hipStream_t s) {
     constexpr int GPB = kBlock / LPR;
     const int64_t blocks = (a.B + GPB - 1) / GPB;
@@ -572,34 +492,6 @@ int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, co
         default: return fail(LGCN_E_UNSUPPORTED, "lgcn_flagged_rows_add: d=%d", d);
     }
 #undef LGCN_FRA
-}
-
-int lgcn_sort_keys_small(const int64_t* keys, int64_t B, int64_t key_offset, uint64_t* sorted, lgcn_stream_t stream) {
-    if (B < 0 || B > kSmallSort || (B > 0 && (!keys || !sorted)))
-        return fail(LGCN_E_ARG, "lgcn_sort_keys_small: B=%lld (max %d)", (long long)B, kSmallSort);
-    if (B == 0) return LGCN_OK;
-    k_sort_small<<<1, 1024, 0, as_stream(stream)>>>(keys, B, key_offset,
-                                                    reinterpret_cast<unsigned long long*>(sorted));
-    return check_launch("k_sort_small");
-}
-
-int lgcn_sorted_segment_add(const uint64_t* sorted, int64_t B, const float* C, int32_t d, float* out_lo,
-                            float* out_hi, int64_t split, float mul, float div, lgcn_stream_t stream) {
-    if (B < 0 || d <= 0 || (B > 0 && (!sorted || !C || !out_lo))) return fail(LGCN_E_ARG, "lgcn_sorted_segment_add: bad args");
-    if (B == 0) return LGCN_OK;
-    if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)))
-        return fail(LGCN_E_UNSUPPORTED, "lgcn_sorted_segment_add: needs d %% 4 == 0 and aligned rows");
-    const auto* w = reinterpret_cast<const unsigned long long*>(sorted);
-    hipStream_t s = as_stream(stream);
-    switch (d) {
-        case 16: return launch_ssa<4, 1>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
-        case 32: return launch_ssa<8, 1>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
-        case 64: return launch_ssa<16, 1>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
-        case 128: return launch_ssa<32, 1>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
-        case 256: return launch_ssa<64, 1>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
-        case 512: return launch_ssa<64, 2>(w, B, C, d, out_lo, out_hi, split, mul, div, s);
-        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_sorted_segment_add: d=%d", d);
-    }
 }
 
 int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* loss, lgcn_stream_t stream) {

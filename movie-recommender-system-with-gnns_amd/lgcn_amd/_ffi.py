@@ -57,11 +57,9 @@ _SIGS = {
                        ctypes.c_int),
     "lgcn_bpr_loss": ([_vp, _i64, _i32, _f32, _vp, _vp], ctypes.c_int),
     "lgcn_segment_rows": ([_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _i32, _f32, _f32, _vp], ctypes.c_int),
-    "lgcn_sort_keys_small": ([_vp, _i64, _i64, _vp, _vp], ctypes.c_int),
     "lgcn_range_scatter_add": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp],
                                ctypes.c_int),
     "lgcn_flagged_rows_add": ([_vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _i64, _vp], ctypes.c_int),
-    "lgcn_sorted_segment_add": ([_vp, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_grad_norm_workspace_floats": ([], ctypes.c_int),
     "lgcn_grad_norm": ([_vp, _i32, _f32, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_adam_step": ([_vp, _i32, _f32, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _i32, _vp], ctypes.c_int),
