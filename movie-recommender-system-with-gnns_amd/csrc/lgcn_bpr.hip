@@ -227,17 +227,21 @@ __global__ __launch_bounds__(kBlock) void k_segment_rows(const int64_t* __restri
 // deterministic, no atomics; each workgroup reads the B keys once (L2-resident).
 constexpr int kRangeCap = 4096;
 
+constexpr int kRSBlock = 1024;          // 16 waves: more lane groups for the per-row sums
+constexpr int kRSWaves = kRSBlock / 64;
+constexpr int kRSChunks = 4;            // 64-key chunks per wave per round (coalesced)
+
 template <int LPR, int NV>
-__global__ __launch_bounds__(kBlock) void k_range_scatter(const int64_t* __restrict__ keys, int64_t B, int64_t nrows,
-                                                          int64_t span, int64_t key_offset, const float* __restrict__ C,
-                                                          int32_t d, float* out_lo, float* out_hi, int64_t split,
-                                                          float mul, float div, const float* __restrict__ C2,
-                                                          float* __restrict__ c2buf, uint8_t* __restrict__ c2flag,
-                                                          int* __restrict__ overflow) {
-    constexpr int GPB = kBlock / LPR;
+__global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __restrict__ keys, int64_t B, int64_t nrows,
+                                                            int64_t span, int64_t key_offset, const float* __restrict__ C,
+                                                            int32_t d, float* out_lo, float* out_hi, int64_t split,
+                                                            float mul, float div, const float* __restrict__ C2,
+                                                            float* __restrict__ c2buf, uint8_t* __restrict__ c2flag,
+                                                            int* __restrict__ overflow) {
+    constexpr int GPB = kRSBlock / LPR;
     __shared__ int lkey[kRangeCap];
     __shared__ int lidx[kRangeCap];
-    __shared__ int wave_cnt[kBlock / 64];
+    __shared__ int wave_cnt[kRSWaves];
     __shared__ int list_n;
     const int64_t lo = int64_t(blockIdx.x) * span;
     const int64_t hi = lo + span < nrows ? lo + span : nrows;
@@ -245,53 +249,52 @@ __global__ __launch_bounds__(kBlock) void k_range_scatter(const int64_t* __restr
     const int wv = threadIdx.x >> 6;
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
+    const unsigned long long below = (1ull << lane) - 1ull;
     if (threadIdx.x == 0) list_n = 0;
     __syncthreads();
     int64_t base = 0;
-    constexpr int KPT = 16;  // keys per thread per round: thread t owns b = base + t*KPT + j
+    constexpr int64_t kPerRound = int64_t(kRSBlock) * kRSChunks;  // <= kRangeCap: a round always fits an empty list
+    static_assert(kPerRound <= kRangeCap, "a round must fit an empty list");
     while (true) {
-        // fill the list (ordered) until full or all keys seen
-        for (; base < B; base += int64_t(kBlock) * KPT) {
+        // fill the list in b order until full or all keys seen: wave w owns keys
+        // [base + w*64*kRSChunks, +64*kRSChunks) of the round, chunk j at + j*64 + lane (coalesced);
+        // order inside a wave comes from the ballot masks, across waves from the wave counts
+        for (; base < B; base += kPerRound) {
+            int64_t kv[kRSChunks];
+            unsigned long long m[kRSChunks];
             int c = 0;
-            unsigned short hit = 0;
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const int64_t bj = base + int64_t(threadIdx.x) * KPT + j;
-                if (bj < B) {
-                    const int64_t key = keys[bj];
-                    if (key >= lo && key < hi) {
-                        hit |= static_cast<unsigned short>(1u << j);
-                        ++c;
-                    }
-                }
+            for (int j = 0; j < kRSChunks; ++j) {
+                const int64_t bj = base + (int64_t(wv) * kRSChunks + j) * 64 + lane;
+                kv[j] = bj < B ? keys[bj] : -1;
             }
-            // ordered block-wide exclusive scan of c (thread order == b order)
-            int incl = c;
 #pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int v = __shfl_up(incl, off, 64);
-                if (lane >= off) incl += v;
+            for (int j = 0; j < kRSChunks; ++j) {
+                m[j] = __ballot(kv[j] >= lo && kv[j] < hi);
+                c += __popcll(m[j]);
             }
-            if (lane == 63) wave_cnt[wv] = incl;
+            if (lane == 0) wave_cnt[wv] = c;
             __syncthreads();
             int off = list_n;
-            for (int w = 0; w < wv; ++w) off += wave_cnt[w];
-            off += incl - c;
             int total = list_n;
-            for (int w = 0; w < kBlock / 64; ++w) total += wave_cnt[w];
+            for (int w = 0; w < kRSWaves; ++w) {
+                const int cw = wave_cnt[w];
+                if (w < wv) off += cw;
+                total += cw;
+            }
             if (total > kRangeCap) {  // this round does not fit: flush first, redo it
                 if (threadIdx.x == 0 && overflow) *overflow = 1;  // C2 rows would then be split: report
                 __syncthreads();
                 break;
             }
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                if (hit & (1u << j)) {
-                    const int64_t bj = base + int64_t(threadIdx.x) * KPT + j;
-                    lkey[off] = static_cast<int>(keys[bj] - lo);
-                    lidx[off] = static_cast<int>(bj);
-                    ++off;
+            for (int j = 0; j < kRSChunks; ++j) {
+                if ((m[j] >> lane) & 1ull) {
+                    const int pos = off + __popcll(m[j] & below);
+                    lkey[pos] = static_cast<int>(kv[j] - lo);
+                    lidx[pos] = static_cast<int>(base + (int64_t(wv) * kRSChunks + j) * 64 + lane);
                 }
+                off += __popcll(m[j]);
             }
             __syncthreads();
             if (threadIdx.x == 0) list_n = total;
@@ -389,7 +392,7 @@ int launch_rs(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset,
     if (C2) {
         if (int rc = check_hip(hipMemsetAsync(c2flag, 0, static_cast<size_t>(B), s), "memset c2flag")) return rc;
     }
-    k_range_scatter<LPR, NV><<<dim3(static_cast<unsigned>(grid)), kBlock, 0, s>>>(keys, B, nrows, span, key_offset, C, d,
+    k_range_scatter<LPR, NV><<<dim3(static_cast<unsigned>(grid)), kRSBlock, 0, s>>>(keys, B, nrows, span, key_offset, C, d,
                                                                                  lo, hi, split, mul, div, C2, c2buf,
                                                                                  c2flag, overflow);
     return check_launch("k_range_scatter");

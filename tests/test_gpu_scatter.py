@@ -1,0 +1,97 @@
+"""The per-step negatives scatter (lgcn_range_scatter_add + lgcn_flagged_rows_add) against a
+sequential CPU restatement: out[off + key[b]] += (Σ_b in b order C[b]) * mul / div, and the
+parked second-source sums Σ_b C2[b] per row. Bit-exact for in-capacity inputs (same b-order
+fp32 sums, mul-then-div), and the overflow flag for concentrated keys."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_scatter(keys, C, out, off, mul, div):
+    out = out.copy()
+    rows = {}
+    for b, k in enumerate(keys):  # first-occurrence order does not matter; per-row order is b order
+        rows.setdefault(int(k), []).append(b)
+    sums = {}
+    for k, bs in rows.items():
+        acc = np.zeros(C.shape[1], np.float32)
+        for b in bs:
+            acc = (acc + C[b]).astype(np.float32)
+        sums[k] = acc
+        out[off + k] = out[off + k] + (acc * np.float32(mul)) / np.float32(div)
+    return out, rows
+
+
+def _run(gpu, keys_np, nrows, off, d, N, mul, div, with_c2=True, seed=0):
+    from lgcn_amd import _ffi
+
+    lib = _ffi.load()
+    rng = np.random.default_rng(seed)
+    B = keys_np.size
+    C = rng.standard_normal((B, d)).astype(np.float32)
+    C2 = rng.standard_normal((B, d)).astype(np.float32)
+    out0 = rng.standard_normal((N, d)).astype(np.float32)
+    split = off + nrows // 2  # two tables, split inside the key range
+    lo = torch.from_numpy(out0[:split].copy()).to(gpu)
+    hi = torch.from_numpy(out0[split:].copy()).to(gpu)
+    keys = torch.from_numpy(keys_np.astype(np.int64)).to(gpu)
+    Cg, C2g = torch.from_numpy(C).to(gpu), torch.from_numpy(C2).to(gpu)
+    buf = torch.empty((max(B, 1), d), dtype=torch.float32, device=gpu)
+    flag = torch.empty(max(B, 1), dtype=torch.uint8, device=gpu)
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    s = _ffi.stream_of(gpu)
+    _ffi.check(lib.lgcn_range_scatter_add(keys.data_ptr(), B, nrows, off, Cg.data_ptr(), d, lo.data_ptr(),
+                                          hi.data_ptr(), split, mul, div,
+                                          C2g.data_ptr() if with_c2 else None, buf.data_ptr(), flag.data_ptr(),
+                                          ovf.data_ptr(), s), "lgcn_range_scatter_add")
+    after1 = torch.cat([lo, hi]).cpu().numpy()
+    if with_c2:
+        _ffi.check(lib.lgcn_flagged_rows_add(keys.data_ptr(), B, off, buf.data_ptr(), flag.data_ptr(), d,
+                                             lo.data_ptr(), hi.data_ptr(), split, s), "lgcn_flagged_rows_add")
+    after2 = torch.cat([lo, hi]).cpu().numpy()
+    return C, C2, out0, after1, after2, int(ovf.item()), flag.cpu().numpy()[:B]
+
+
+@pytest.mark.parametrize("B,nrows,d", [(1, 7, 64), (1000, 500, 64), (10000, 59047, 128), (30000, 5000, 64),
+                                       (4000, 300000, 32), (2000, 1000, 256)])
+def test_range_scatter_matches_sequential(gpu, B, nrows, d):
+    rng = np.random.default_rng(B + nrows)
+    keys = rng.integers(0, nrows, B)
+    off = 11
+    N = off + nrows + 3
+    mul, div = float(np.float32(1 / 4)), 4.0
+    C, C2, out0, after1, after2, ovf, flag = _run(gpu, keys, nrows, off, d, N, mul, div)
+    assert ovf == 0
+    ref1, rows = _ref_scatter(keys, C, out0, off, mul, div)
+    np.testing.assert_array_equal(after1, ref1)
+    ref2, _ = _ref_scatter(keys, C2, ref1, off, 1.0, 1.0)
+    np.testing.assert_array_equal(after2, ref2)
+    # exactly one flagged slot per distinct row: its first occurrence
+    firsts = sorted(bs[0] for bs in rows.values())
+    np.testing.assert_array_equal(np.nonzero(flag)[0], firsts)
+
+
+def test_range_scatter_empty_and_single_row(gpu):
+    # B = 0 is a no-op
+    C, C2, out0, after1, after2, ovf, _ = _run(gpu, np.zeros(0, np.int64), 10, 0, 64, 10, 1.0, 1.0)
+    np.testing.assert_array_equal(after2, out0)
+    # every key the same row (well inside capacity): one sum in b order
+    keys = np.full(3000, 5)
+    C, C2, out0, after1, after2, ovf, flag = _run(gpu, keys, 10, 0, 64, 10, 1.0, 3.0)
+    assert ovf == 0
+    ref1, _ = _ref_scatter(keys, C, out0, 0, 1.0, 3.0)
+    np.testing.assert_array_equal(after1, ref1)
+    assert flag.sum() == 1 and flag[0] == 1
+
+
+def test_range_scatter_overflow_is_reported(gpu):
+    # > 4096 keys in one workgroup's range: the dF part stays correct (flushed partial sums,
+    # within rounding), and the overflow flag tells the caller the parked sums were split
+    rng = np.random.default_rng(3)
+    keys = rng.integers(0, 4, 9000)
+    C, C2, out0, after1, _, ovf, _ = _run(gpu, keys, 100000, 0, 64, 100000, 1.0, 1.0, with_c2=False)
+    ref1, _ = _ref_scatter(keys, C, out0, 0, 1.0, 1.0)
+    np.testing.assert_allclose(after1, ref1, rtol=1e-5, atol=1e-4)
+    assert ovf == 1
