@@ -228,6 +228,38 @@ int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, co
                           lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Recall@k (reference utils/train_test.py:165-212, compute_recall_at_k, called from evaluate
+ * :136-163): per sampled user row, the number of positives (candidate index < P) among the
+ * top-k cosine scores against all M = P + P' candidate rows, without the [Q, M] score matrix.
+ *   lgcn_recall_width: D = padded width the kernels use for d (a power of two >= 8, d <= 256)
+ *     and the multiple Q must be padded to.
+ *   lgcn_normalize_rows: out[r, :D] = x[idx ? idx[r] : r, :d] / ||.||_2, zero-padded columns;
+ *     rows in [rows, out_rows) are zero (query padding).
+ *   lgcn_score_filter: f32 MFMA scores of Q queries vs candidates r*stride (r < M); thr == NULL
+ *     writes every score at slot r of each query's list (dense mode, M <= cap), otherwise keys
+ *     >= thr[q] are appended (list_n[q] += 1; caller zeroes list_n; overflow past cap is
+ *     counted but not stored).
+ *   lgcn_select_topk: per query, the k-th largest key of its list (dense_n entries when list_n
+ *     is NULL) -> thr_out[q]; and/or hits_out[q] = positives ranked in the top k (ties take the
+ *     lowest candidate index first), -1 if the list holds fewer than k entries.
+ * Keys are order-preserving uint32 images of the f32 scores (NaN highest). */
+int lgcn_recall_width(int32_t d, int32_t* D_out, int32_t* qpad_multiple);
+int lgcn_normalize_rows(const float* x, const int64_t* idx, int64_t rows, int64_t ld, int32_t d, float* out,
+                        int32_t D, int64_t out_rows, lgcn_stream_t stream);
+int lgcn_score_filter(const float* Qn, int64_t Qpad, int64_t Qvalid, const float* Cn, int64_t M, int64_t stride,
+                      int32_t D, const uint32_t* thr, uint32_t* list_key, int32_t* list_idx, int32_t* list_n,
+                      int32_t cap, lgcn_stream_t stream);
+int lgcn_select_topk(const uint32_t* list_key, const int32_t* list_idx, const int32_t* list_n, int32_t dense_n,
+                     int32_t cap, int32_t k, int64_t P, int64_t Qpad, int64_t Qvalid, uint32_t* thr_out,
+                     int32_t* hits_out, lgcn_stream_t stream);
+
+/* Host-only (no GPU): `draws` consecutive numpy legacy np.random.choice(n, size, replace=False)
+ * calls (reference utils/train_test.py:187) on the MT19937 state (key[624], *pos) of
+ * np.random.get_state(), written to out[draws*size]; key/pos are advanced exactly as numpy would
+ * advance them, so np.random.set_state() with them continues the caller's stream unchanged. */
+int lgcn_legacy_choice(uint32_t* key, int32_t* pos, int64_t n, int64_t size, int64_t draws, int64_t* out);
+
+/* ---------------------------------------------------------------------------------------
  * Training-step tail (reference utils/train_test.py:95-96: clip_grad_norm_(max_norm=1) then
  * optim.Adam(lr=1e-3).step() over the two dense embedding tables). Device pointers; the
  * tensor descriptors themselves are a host array of n (<= 8) entries.

@@ -1,0 +1,402 @@
+// Recall@k of the reference's evaluate() (reference utils/train_test.py:165-212) on gfx950.
+//
+// The reference scores sample_size sampled "user" rows against every positive and negative row
+// of the edge set (cosine = mm of L2-normalised rows), takes torch.topk(k) per user and counts
+// the hits that are positives (index < P). Per user, that count is all we need, so nothing of
+// the [Q, M] score matrix is kept:
+//
+//   k_normalize_rows  x[r] / ||x[r]|| (optionally gathered through an index list), written into a
+//                     zero-padded [rows, D] image (D = the compiled width >= d);
+//   k_score_filter    f32 MFMA (v_mfma_f32_32x32x2_f32, exact f32) scores of 32-query blocks
+//                     against 32-candidate blocks; an epilogue keeps (key, index) of every score
+//                     at or above the query's threshold key in a per-query list;
+//   k_select_topk     one workgroup per query: radix select (4 x 8-bit passes) of the k-th
+//                     largest key in its list, then either that key (a new threshold) or the
+//                     hit count (positives above it, plus positives among the ties).
+//
+// Thresholds come from a strided candidate subset first: the k-th largest score of ANY subset is
+// <= the k-th largest of all M, so the filtered list always holds the true top k, and it holds
+// about k * M / |subset| entries. If a list overflows its capacity, its kept entries are real
+// candidates too, so their k-th largest is again a valid (tighter) threshold and the caller
+// re-runs the filter (lgcn_amd.recall does this; it never happens at the reference's sizes).
+//
+// Ties at the k-th score take the lowest candidate indices first, which are the positives
+// (torch.topk leaves tie order unspecified). NaN scores (zero rows, normalised as 0/0 like the
+// reference) rank first, as torch.topk ranks NaN above every number.
+
+#include "lgcn_common.h"
+
+using namespace lgcn;
+
+namespace {
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+__device__ __forceinline__ uint32_t score_key(float s) {
+    if (s != s) return 0xFFFFFFFFu;
+    const uint32_t u = __float_as_uint(s);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// one 32-lane half-wave per row
+__global__ __launch_bounds__(kBlock) void k_normalize_rows(const float* __restrict__ x, const int64_t* __restrict__ idx,
+                                                           int64_t rows, int64_t ld, int32_t d,
+                                                           float* __restrict__ out, int32_t D, int64_t out_rows) {
+    const int64_t r = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / 32;
+    const int l = threadIdx.x & 31;
+    if (r >= out_rows) return;
+    float* o = out + r * D;
+    if (r >= rows) {  // padding rows: zeros
+        for (int c = l; c < D; c += 32) o[c] = 0.f;
+        return;
+    }
+    const float* src = x + (idx ? idx[r] : r) * ld;
+    float ss = 0.f;
+    for (int c = l; c < d; c += 32) {
+        const float v = src[c];
+        ss += v * v;
+    }
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 32);
+    const float n = sqrtf(ss);
+    for (int c = l; c < D; c += 32) o[c] = (c < d) ? src[c] / n : 0.f;
+}
+
+constexpr int kStage = 512;  // staged accepted scores per wave
+
+// Workgroup = 4 waves over the same candidate blocks; wave w owns the 32 queries
+// [(qg*4 + w)*32, +32), held in registers for the whole launch. Lane l = (i = l&31, h = l>>5)
+// holds, for MFMA step s, A = Q[i][h*D/2 + s] and B = C[j][h*D/2 + s], so each step's 2-wide k
+// slice is columns s and D/2+s and the D/2 steps cover the row.
+// Candidate blocks (32 rows) are staged through LDS, double-buffered: the global loads of block
+// n+1 are in flight (in registers) while block n's MFMAs run, and land in the other buffer.
+// Grid: 1-D, XCD-aware. Workgroup wid runs on XCD wid % 8; the query groups of one candidate
+// chunk get consecutive slots of the SAME XCD, so they run together and share its L2 copy of the
+// chunk's rows (the queries, not the candidates, are what differs between them).
+// At <= 170 VGPRs two waves share each SIMD, so one wave's epilogue hides under the other's MFMAs.
+template <int D>
+__global__ __launch_bounds__(kBlock, 2) void k_score_filter(const float* __restrict__ Qn, int64_t Qvalid, int32_t nqg,
+                                                            int32_t nchunk, const float* __restrict__ Cn, int64_t M,
+                                                            int64_t stride, const uint32_t* __restrict__ thr,
+                                                            uint32_t* __restrict__ list_key,
+                                                            int32_t* __restrict__ list_idx,
+                                                            int32_t* __restrict__ list_n, int32_t cap) {
+    constexpr int H = D / 2;
+    constexpr int ROWF = D + 4;               // padded LDS row: conflict-free ds_read_b128 down a column
+    constexpr int NF4 = 32 * D / 4;           // float4s per candidate block
+    constexpr int PER = (NF4 + kBlock - 1) / kBlock;
+    __shared__ float cs[2][32 * ROWF];
+    // wave-private staging of accepted scores: appended without atomics (ballot prefix), flushed
+    // to the per-query lists with ONE returning global atomic per query per flush
+    __shared__ uint32_t st_key[4][kStage];
+    __shared__ int32_t st_idx[4][kStage];
+    __shared__ uint32_t st_qr[4][kStage];  // query row | rank-within-query << 8
+    __shared__ int32_t st_qcnt[4][32];
+    __shared__ int32_t st_qbase[4][32];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int i = lane & 31;
+    const int h = lane >> 5;
+    const int wid = blockIdx.x;
+    const int slot = wid >> 3;
+    const int qg = slot % nqg;
+    const int chunk = (slot / nqg) * 8 + (wid & 7);
+    const int64_t q0 = (int64_t(qg) * 4 + wv) * 32;  // first query of this wave
+    float a[H];
+    {
+        const float4* src = reinterpret_cast<const float4*>(Qn + (q0 + i) * D + h * H);
+#pragma unroll
+        for (int v = 0; v < H / 4; ++v) {
+            const float4 t = src[v];
+            a[4 * v] = t.x;
+            a[4 * v + 1] = t.y;
+            a[4 * v + 2] = t.z;
+            a[4 * v + 3] = t.w;
+        }
+    }
+    // this lane's 16 output rows: (r&3) + 8*(r>>2) + 4h; padding queries get a key no score
+    // reaches (their rows are zero, so their scores are 0, never NaN)
+    uint32_t th[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t q = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        th[r] = (q < Qvalid) ? (thr ? thr[q] : 0u) : 0xFFFFFFFFu;
+    }
+    if (lane < 32) st_qcnt[wv][lane] = 0;
+    int scnt = 0;  // wave-uniform staged count
+    const unsigned long long below = (1ull << lane) - 1ull;
+    auto flush = [&]() {  // wave-uniform
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane < 32) {
+            const int c = st_qcnt[wv][lane];
+            st_qbase[wv][lane] = c > 0 ? atomicAdd(list_n + q0 + lane, c) : 0;
+            st_qcnt[wv][lane] = 0;
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        for (int e = lane; e < scnt; e += 64) {
+            const uint32_t qr = st_qr[wv][e];
+            const int row = static_cast<int>(qr & 255u);
+            const int32_t pos = st_qbase[wv][row] + static_cast<int32_t>(qr >> 8);
+            if (pos < cap) {
+                const int64_t q = q0 + row;
+                list_key[q * cap + pos] = st_key[wv][e];
+                list_idx[q * cap + pos] = st_idx[wv][e];
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        scnt = 0;
+    };
+    const int64_t nblk = (M + 31) / 32;
+    float4 pre[PER];
+    auto fetch = [&](int64_t cb) {
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+            const int t = threadIdx.x + p * kBlock;
+            const int r = t / (D / 4), c4 = t % (D / 4);
+            const int64_t j = cb * 32 + r;
+            pre[p] = (t < NF4 && j < M) ? reinterpret_cast<const float4*>(Cn + j * stride * D)[c4]
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto land = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+            const int t = threadIdx.x + p * kBlock;
+            if (t < NF4) *reinterpret_cast<float4*>(&cs[buf][(t / (D / 4)) * ROWF + (t % (D / 4)) * 4]) = pre[p];
+        }
+    };
+    int64_t cb = chunk;
+    if (cb < nblk) {
+        fetch(cb);
+        land(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (; cb < nblk; cb += nchunk) {
+        const int64_t nxt = cb + nchunk;
+        if (nxt < nblk) fetch(nxt);  // in flight during this block's MFMAs
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        const float* brow = &cs[buf][i * ROWF + h * H];
+#pragma unroll
+        for (int v = 0; v < H / 4; ++v) {
+            const float4 bv = *reinterpret_cast<const float4*>(brow + 4 * v);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v], bv.x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v + 1], bv.y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v + 2], bv.z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v + 3], bv.w, acc, 0, 0, 0);
+        }
+        // epilogue: column = candidate j (this lane's), rows = queries; branch-free test, and
+        // a wave-uniform branch only for the (rare) slots where some lane passes
+        const int64_t j = cb * 32 + i;
+        const int32_t jj = static_cast<int32_t>(j * stride);
+        const bool jok = j < M;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row0 = (r & 3) + 8 * (r >> 2);
+            const int row = row0 + 4 * h;
+            const uint32_t key = score_key(acc[r]);
+            const bool take = jok & (key >= th[r]);
+            if (thr == nullptr) {  // dense mode: every subset score at its subset slot
+                if (take) {
+                    const int64_t q = q0 + row;
+                    list_key[q * cap + j] = key;
+                    list_idx[q * cap + j] = jj;
+                }
+                continue;
+            }
+            const unsigned long long m = __ballot(take);
+            if (m == 0ull) continue;
+            const int n = __popcll(m);
+            if (scnt + n > kStage) flush();
+            const unsigned lo = static_cast<unsigned>(m), hi = static_cast<unsigned>(m >> 32);
+            const int c0 = st_qcnt[wv][row0], c1 = st_qcnt[wv][row0 + 4];
+            if (take) {
+                const int sl = scnt + __popcll(m & below);
+                const unsigned half = h ? hi : lo;
+                const int rank = (h ? c1 : c0) + __popc(half & static_cast<unsigned>(below >> (32 * h)));
+                st_key[wv][sl] = key;
+                st_idx[wv][sl] = jj;
+                st_qr[wv][sl] = static_cast<uint32_t>(row) | (static_cast<uint32_t>(rank) << 8);
+            }
+            if (lane == 0) {
+                st_qcnt[wv][row0] = c0 + __popc(lo);
+                st_qcnt[wv][row0 + 4] = c1 + __popc(hi);
+            }
+            scnt += n;
+        }
+        if (nxt < nblk) land(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    if (thr != nullptr) flush();
+}
+
+// k-th largest key per query list (radix select), then the threshold or the hit count.
+constexpr int kSelBlock = 1024;
+
+__global__ __launch_bounds__(kSelBlock) void k_select_topk(const uint32_t* __restrict__ list_key,
+                                                           const int32_t* __restrict__ list_idx,
+                                                           const int32_t* __restrict__ list_n, int32_t dense_n,
+                                                           int32_t cap, int32_t k, int64_t P, int64_t Qvalid,
+                                                           uint32_t* __restrict__ thr_out, int32_t* __restrict__ hits_out) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t s_prefix, s_mask, s_k;
+    __shared__ int32_t red[kSelBlock / 64][2];
+    const int64_t q = blockIdx.x;
+    if (q >= Qvalid) {
+        if (threadIdx.x == 0) {
+            if (thr_out) thr_out[q] = 0xFFFFFFFFu;
+            if (hits_out) hits_out[q] = 0;
+        }
+        return;
+    }
+    int32_t n = list_n ? list_n[q] : dense_n;
+    if (n > cap) n = cap;
+    const uint32_t* keys = list_key + q * cap;
+    const int32_t* idx = list_idx + q * cap;
+    if (n < k) {  // cannot rank k: threshold "everything", hits invalid
+        if (threadIdx.x == 0) {
+            if (thr_out) thr_out[q] = 0u;
+            if (hits_out) hits_out[q] = -1;
+        }
+        return;
+    }
+    if (threadIdx.x == 0) {
+        s_prefix = 0u;
+        s_mask = 0u;
+        s_k = static_cast<uint32_t>(k);
+    }
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int t = threadIdx.x; t < 256; t += kSelBlock) hist[t] = 0u;
+        __syncthreads();
+        const uint32_t prefix = s_prefix, mask = s_mask;
+        for (int e = threadIdx.x; e < n; e += kSelBlock) {
+            const uint32_t key = keys[e];
+            if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t cum = 0, kk = s_k;
+            int bsel = 0;
+            for (int bin = 255; bin >= 0; --bin) {
+                if (cum + hist[bin] >= kk) {
+                    bsel = bin;
+                    break;
+                }
+                cum += hist[bin];
+            }
+            s_k = kk - cum;
+            s_prefix = prefix | (static_cast<uint32_t>(bsel) << shift);
+            s_mask = mask | (255u << shift);
+        }
+        __syncthreads();
+    }
+    const uint32_t T = s_prefix;
+    const int32_t need = static_cast<int32_t>(s_k);  // taken from the keys equal to T
+    if (thr_out && threadIdx.x == 0) thr_out[q] = T;
+    if (!hits_out) return;
+    int32_t above = 0, ties = 0;
+    for (int e = threadIdx.x; e < n; e += kSelBlock) {
+        const uint32_t key = keys[e];
+        const bool pos = idx[e] < P;
+        above += (key > T && pos) ? 1 : 0;
+        ties += (key == T && pos) ? 1 : 0;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        above += __shfl_xor(above, off, 64);
+        ties += __shfl_xor(ties, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6][0] = above;
+        red[threadIdx.x >> 6][1] = ties;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t A = 0, Ti = 0;
+        for (int w = 0; w < kSelBlock / 64; ++w) {
+            A += red[w][0];
+            Ti += red[w][1];
+        }
+        hits_out[q] = A + (Ti < need ? Ti : need);
+    }
+}
+
+template <int D>
+int launch_filter(const float* Qn, int64_t Qpad, int64_t Qvalid, const float* Cn, int64_t M, int64_t stride,
+                  const uint32_t* thr, uint32_t* lk, int32_t* li, int32_t* ln, int32_t cap, hipStream_t s) {
+    constexpr int QW = 4 * 32;  // queries per workgroup
+    if (Qpad % QW != 0) return fail(LGCN_E_ARG, "lgcn_score_filter: padded query count %lld not a multiple of %d",
+                                    (long long)Qpad, QW);
+    const int64_t nblk = (M + 31) / 32;
+    const int64_t nqg = Qpad / QW;
+    // candidate chunks: a multiple of 8 (the XCD mapping), ~2048 workgroups in all
+    int64_t nchunk = (2048 / nqg + 7) / 8 * 8;
+    const int64_t need = (nblk + 7) / 8 * 8;
+    if (nchunk > need) nchunk = need;
+    if (nchunk < 8) nchunk = 8;
+    const int64_t grid = nqg * nchunk;
+    if (grid > INT32_MAX || nqg > INT32_MAX) return fail(LGCN_E_ARG, "lgcn_score_filter: too many queries");
+    k_score_filter<D><<<dim3(static_cast<unsigned>(grid)), kBlock, 0, s>>>(
+        Qn, Qvalid, static_cast<int32_t>(nqg), static_cast<int32_t>(nchunk), Cn, M, stride, thr, lk, li, ln, cap);
+    return check_launch("k_score_filter");
+}
+
+}  // namespace
+
+extern "C" {
+
+int lgcn_recall_width(int32_t d, int32_t* D_out, int32_t* qpad_multiple) {
+    if (d <= 0 || d > 256 || !D_out) return fail(LGCN_E_UNSUPPORTED, "lgcn_recall_width: d=%d (max 256)", d);
+    int D = 8;
+    while (D < d) D <<= 1;
+    *D_out = D;
+    if (qpad_multiple) *qpad_multiple = 128;
+    return LGCN_OK;
+}
+
+int lgcn_normalize_rows(const float* x, const int64_t* idx, int64_t rows, int64_t ld, int32_t d, float* out,
+                        int32_t D, int64_t out_rows, lgcn_stream_t stream) {
+    if (rows < 0 || out_rows < rows || d <= 0 || D < d || ld < d || (out_rows > 0 && !out) || (rows > 0 && !x))
+        return fail(LGCN_E_ARG, "lgcn_normalize_rows: bad args");
+    if (out_rows == 0) return LGCN_OK;
+    const int64_t threads = out_rows * 32;
+    k_normalize_rows<<<grid_for(threads, kBlock, int64_t(1) << 31), kBlock, 0, as_stream(stream)>>>(x, idx, rows, ld, d,
+                                                                                                   out, D, out_rows);
+    return check_launch("k_normalize_rows");
+}
+
+int lgcn_score_filter(const float* Qn, int64_t Qpad, int64_t Qvalid, const float* Cn, int64_t M, int64_t stride,
+                      int32_t D, const uint32_t* thr, uint32_t* list_key, int32_t* list_idx, int32_t* list_n,
+                      int32_t cap, lgcn_stream_t stream) {
+    if (!Qn || Qpad <= 0 || Qvalid > Qpad || M < 0 || stride <= 0 || !list_key || !list_idx || cap <= 0 ||
+        (thr && !list_n) || (M > 0 && !Cn) || (M - 1) * stride >= (int64_t(1) << 31))
+        return fail(LGCN_E_ARG, "lgcn_score_filter: bad args");
+    if (!thr && M > cap) return fail(LGCN_E_ARG, "lgcn_score_filter: dense mode needs M <= cap");
+    if (M == 0) return LGCN_OK;
+    hipStream_t s = as_stream(stream);
+    switch (D) {
+        case 8: return launch_filter<8>(Qn, Qpad, Qvalid, Cn, M, stride, thr, list_key, list_idx, list_n, cap, s);
+        case 16: return launch_filter<16>(Qn, Qpad, Qvalid, Cn, M, stride, thr, list_key, list_idx, list_n, cap, s);
+        case 32: return launch_filter<32>(Qn, Qpad, Qvalid, Cn, M, stride, thr, list_key, list_idx, list_n, cap, s);
+        case 64: return launch_filter<64>(Qn, Qpad, Qvalid, Cn, M, stride, thr, list_key, list_idx, list_n, cap, s);
+        case 128: return launch_filter<128>(Qn, Qpad, Qvalid, Cn, M, stride, thr, list_key, list_idx, list_n, cap, s);
+        case 256: return launch_filter<256>(Qn, Qpad, Qvalid, Cn, M, stride, thr, list_key, list_idx, list_n, cap, s);
+        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_score_filter: D=%d (use lgcn_recall_width)", D);
+    }
+}
+
+int lgcn_select_topk(const uint32_t* list_key, const int32_t* list_idx, const int32_t* list_n, int32_t dense_n,
+                     int32_t cap, int32_t k, int64_t P, int64_t Qpad, int64_t Qvalid, uint32_t* thr_out,
+                     int32_t* hits_out, lgcn_stream_t stream) {
+    if (!list_key || !list_idx || cap <= 0 || k <= 0 || Qpad <= 0 || Qvalid > Qpad || (!thr_out && !hits_out) ||
+        (!list_n && dense_n < 0))
+        return fail(LGCN_E_ARG, "lgcn_select_topk: bad args");
+    k_select_topk<<<dim3(static_cast<unsigned>(Qpad)), kSelBlock, 0, as_stream(stream)>>>(
+        list_key, list_idx, list_n, dense_n, cap, k, P, Qvalid, thr_out, hits_out);
+    return check_launch("k_select_topk");
+}
+
+}  // extern "C"

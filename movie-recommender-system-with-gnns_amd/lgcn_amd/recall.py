@@ -1,0 +1,135 @@
+"""Recall@k on the GPU: the reference's compute_recall_at_k (utils/train_test.py:165-212) as
+three HIP launches per pass (csrc/lgcn_recall.hip), with no [Q, M] score matrix and one host
+read per call.
+
+    Qn = normalize(users[picked])               lgcn_normalize_rows (gathered, zero-padded)
+    Cn = cat(normalize(pos), normalize(neg))    lgcn_normalize_rows x2
+    thr = k-th best of a strided subset         lgcn_score_filter (dense) + lgcn_select_topk
+    lists = scores >= thr                       lgcn_score_filter (f32 MFMA, all M)
+    hits = positives in the top k               lgcn_select_topk
+
+All num_samples x sample_size sampled users go through one pass (a query's hits do not depend on
+the other queries), and the numpy draws are the reference's own calls in the same order.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _ffi
+
+SUBSET = 16384   # candidates scored for the first thresholds (≈ k·M/SUBSET survive the filter)
+CAP = 16384      # per-query list capacity
+
+
+class _Workspace:
+    def __init__(self):
+        self.key = None
+
+    def get(self, dev, Qpad, M, D, cap):
+        key = (dev, Qpad, M, D, cap)
+        if key != self.key:
+            self.key = key
+            self.Qn = torch.empty((Qpad, D), dtype=torch.float32, device=dev)
+            self.Cn = torch.empty((max(M, 1), D), dtype=torch.float32, device=dev)
+            self.lkey = torch.empty((Qpad, cap), dtype=torch.int32, device=dev)
+            self.lidx = torch.empty((Qpad, cap), dtype=torch.int32, device=dev)
+            self.lcnt = torch.zeros(Qpad, dtype=torch.int32, device=dev)
+            self.thr = torch.empty(Qpad, dtype=torch.int32, device=dev)
+            self.hits = torch.empty(Qpad, dtype=torch.int32, device=dev)
+        return self
+
+
+_WS = _Workspace()
+
+
+def _normalize_into(lib, x: torch.Tensor, idx, rows: int, out_ptr: int, D: int, out_rows: int, stream):
+    if x.dim() != 2 or x.dtype != torch.float32 or x.stride(1) != 1:
+        raise TypeError("recall: embeddings must be 2-D fp32 with unit column stride")
+    _ffi.check(lib.lgcn_normalize_rows(x.data_ptr() if x.numel() else None, idx, rows, x.stride(0), x.shape[1],
+                                       out_ptr, D, out_rows, stream), "lgcn_normalize_rows")
+
+
+def topk_hits(users: torch.Tensor, picked: torch.Tensor, pos: torch.Tensor, neg: torch.Tensor, k: int,
+              cap: int = CAP, subset: int = SUBSET) -> torch.Tensor:
+    """hits[q] = number of positives (rows of ``pos``) among the top-k cosine scores of
+    users[picked[q]] against cat(pos, neg); int32 [Q] on the device."""
+    lib = _ffi.load()
+    dev = users.device
+    for t in (users, pos, neg):
+        _ffi.require_device(t, "recall")
+    d = users.shape[1]
+    if pos.shape[1] != d or neg.shape[1] != d:
+        raise ValueError("recall: users, positives and negatives must have the same width")
+    P, Nn = pos.shape[0], neg.shape[0]
+    M = P + Nn
+    if k > M:
+        raise RuntimeError("selected index k out of range")
+    if k > cap:
+        raise ValueError(f"recall: k={k} exceeds the list capacity {cap}")
+    Dv, qm = ctypes.c_int32(0), ctypes.c_int32(0)
+    _ffi.check(lib.lgcn_recall_width(d, ctypes.byref(Dv), ctypes.byref(qm)), "lgcn_recall_width")
+    D, qmul = Dv.value, qm.value
+    picked = picked.to(device=dev, dtype=torch.int64).contiguous()
+    Q = picked.numel()
+    Qpad = max(qmul, (Q + qmul - 1) // qmul * qmul)
+    ws = _WS.get(dev, Qpad, M, D, cap)
+    s = _ffi.stream_of(dev)
+    _normalize_into(lib, users, picked.data_ptr(), Q, ws.Qn.data_ptr(), D, Qpad, s)
+    _normalize_into(lib, pos, None, P, ws.Cn.data_ptr(), D, P, s)
+    _normalize_into(lib, neg, None, Nn, ws.Cn.data_ptr() + P * D * 4, D, Nn, s)
+    # first thresholds: the k-th best of a strided subset (a lower bound of the true k-th best)
+    stride = max(1, -(-M // min(subset, cap)))
+    S = -(-M // stride)
+    _ffi.check(lib.lgcn_score_filter(ws.Qn.data_ptr(), Qpad, Q, ws.Cn.data_ptr(), S, stride, D, None,
+                                     ws.lkey.data_ptr(), ws.lidx.data_ptr(), None, cap, s), "lgcn_score_filter")
+    _ffi.check(lib.lgcn_select_topk(ws.lkey.data_ptr(), ws.lidx.data_ptr(), None, S, cap, k, P, Qpad, Q,
+                                    ws.thr.data_ptr(), None, s), "lgcn_select_topk")
+    for _ in range(8):
+        ws.lcnt.zero_()
+        _ffi.check(lib.lgcn_score_filter(ws.Qn.data_ptr(), Qpad, Q, ws.Cn.data_ptr(), M, 1, D, ws.thr.data_ptr(),
+                                         ws.lkey.data_ptr(), ws.lidx.data_ptr(), ws.lcnt.data_ptr(), cap, s),
+                   "lgcn_score_filter")
+        if int(ws.lcnt.max().item()) <= cap:
+            _ffi.check(lib.lgcn_select_topk(ws.lkey.data_ptr(), ws.lidx.data_ptr(), ws.lcnt.data_ptr(), 0, cap, k,
+                                            P, Qpad, Q, None, ws.hits.data_ptr(), s), "lgcn_select_topk")
+            return ws.hits[:Q].clone()
+        # a list overflowed: its kept entries are real candidates, so their k-th best is a valid,
+        # tighter threshold; filter again
+        _ffi.check(lib.lgcn_select_topk(ws.lkey.data_ptr(), ws.lidx.data_ptr(), ws.lcnt.data_ptr(), 0, cap, k,
+                                        P, Qpad, Q, ws.thr.data_ptr(), None, s), "lgcn_select_topk")
+    raise RuntimeError("recall: candidate lists kept overflowing (scores too concentrated for the capacity)")
+
+
+def legacy_choice(n: int, size: int, draws: int) -> np.ndarray:
+    """``draws`` consecutive np.random.choice(n, size, replace=False) calls on numpy's global
+    legacy generator (reference utils/train_test.py:187), as one [draws, size] int64 array: the
+    same picks and the same generator state afterwards (lgcn_legacy_choice, host C++)."""
+    state = np.random.get_state()
+    if state[0] != "MT19937" or size > n or n <= 0 or size < 0 or n > 2**31 - 1:
+        return np.stack([np.random.choice(n, size, replace=False) for _ in range(draws)])
+    key = np.array(state[1], dtype=np.uint32)
+    pos = ctypes.c_int32(int(state[2]))
+    out = np.empty((draws, size), dtype=np.int64)
+    _ffi.check(_ffi.load().lgcn_legacy_choice(key.ctypes.data, ctypes.byref(pos), n, size, draws, out.ctypes.data),
+               "lgcn_legacy_choice")
+    np.random.set_state(("MT19937", key, pos.value, state[3], state[4]))
+    return out
+
+
+def compute_recall_at_k(embs, k: int = 20, num_samples: int = 10, sample_size: int = 100) -> float:
+    """The reference's compute_recall_at_k (utils/train_test.py:165-212) on device tensors."""
+    user_embs, pos_item_embs, neg_item_embs = embs
+    num_pos = pos_item_embs.size(0)
+    picked = legacy_choice(user_embs.size(0), sample_size, num_samples).reshape(-1)
+    hits = topk_hits(user_embs, torch.from_numpy(picked), pos_item_embs, neg_item_embs, k)
+    if int(hits.min().item()) < 0:
+        raise RuntimeError("recall: a query ranked fewer than k candidates")
+    per_user = hits.to(torch.float32) / num_pos
+    means = [m for m in per_user.view(num_samples, sample_size).mean(dim=1).double().cpu().tolist()]
+    total = 0.0
+    for m in means:
+        total += m
+    return total / num_samples

@@ -11,7 +11,8 @@ Differences are in where the work runs, not in the numbers:
     device (the same double-precision sums), read once per epoch;
   * Recall@k keeps the reference's numpy sampling (np.random.choice, :187) but labels the top-k
     hits by index (< number of positives) instead of gathering from a [100, 2B] mask — the same
-    0/1 values — and reads the per-sample means back once.
+    0/1 values — and reads the per-sample means back once. On device tensors it runs the HIP
+    kernels of lgcn_amd.recall (all samples in one pass, no [100, 2B] score matrix).
 """
 from typing import Tuple
 
@@ -93,6 +94,10 @@ def compute_recall_at_k(embs, k: int = 20, num_samples: int = 10, sample_size: i
     them against every positive and negative row of the batch, count top-k hits among the
     positives, divide by the number of positives; mean over num_samples draws."""
     user_embs, pos_item_embs, neg_item_embs = embs
+    if user_embs.is_cuda:  # HIP path: f32 MFMA scores + per-user top-k selection, no score matrix
+        from lgcn_amd.recall import compute_recall_at_k as recall_hip
+
+        return recall_hip(embs, k=k, num_samples=num_samples, sample_size=sample_size)
     num_pos = pos_item_embs.size(0)
     candidates = torch.cat((normalize_embedding(pos_item_embs), normalize_embedding(neg_item_embs))).t()
     per_sample = []

@@ -1,0 +1,109 @@
+"""Recall@k on the GPU (lgcn_amd.recall, csrc/lgcn_recall.hip) against the CPU restatement
+oracle/recall_ref.py (pinned to the reference's own compute_recall_at_k outputs in
+tests/test_oracle_recall.py). Hit counts are exact on every query whose k-th and (k+1)-th
+float64 scores are separated by more than fp32 rounding; ties take the positives first on both
+sides."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import recall_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _emb(rng, n, d):
+    return rng.standard_normal((n, d)).astype(np.float32)
+
+
+def _check_hits(gpu, users, pos, neg, picked, k, **kw):
+    from lgcn_amd.recall import topk_hits
+
+    t = lambda a: torch.from_numpy(a).to(gpu)
+    hits = topk_hits(t(users), torch.from_numpy(picked), t(pos), t(neg), k, **kw).cpu().numpy()
+    ref, gap = R.topk_hits(users[picked], pos, neg, k, return_gap=True)
+    sep = gap > 1e-5
+    assert sep.mean() > 0.9
+    np.testing.assert_array_equal(hits[sep], ref[sep])
+    return hits, ref
+
+
+@pytest.mark.parametrize("d", [8, 32, 64, 100, 128, 256])
+@pytest.mark.parametrize("k", [1, 20, 100])
+def test_topk_hits_match_oracle(gpu, d, k):
+    rng = np.random.default_rng(d * 1000 + k)
+    users, pos, neg = _emb(rng, 900, d), _emb(rng, 3000, d), _emb(rng, 2500, d)
+    picked = rng.choice(900, 300, replace=False)
+    _check_hits(gpu, users, pos, neg, picked, k)
+
+
+def test_topk_hits_subset_thresholds_and_overflow(gpu):
+    # M = 60k > SUBSET: strided-subset thresholds; then a tiny capacity forces the overflow loop
+    rng = np.random.default_rng(5)
+    d = 64
+    users, pos, neg = _emb(rng, 500, d), _emb(rng, 30000, d), _emb(rng, 30000, d)
+    picked = rng.choice(500, 256, replace=False)
+    _check_hits(gpu, users, pos, neg, picked, 100)
+    _check_hits(gpu, users, pos, neg, picked, 100, cap=512, subset=512)
+
+
+def test_topk_hits_ties_take_positives_first(gpu):
+    # every negative duplicates a positive: each score appears twice, positives first
+    rng = np.random.default_rng(6)
+    d = 32
+    users, pos = _emb(rng, 200, d), _emb(rng, 400, d)
+    neg = pos[rng.permutation(400)]
+    picked = rng.choice(200, 100, replace=False)
+    from lgcn_amd.recall import topk_hits
+
+    t = lambda a: torch.from_numpy(a).to(gpu)
+    for k in (1, 7, 20):
+        hits = topk_hits(t(users), torch.from_numpy(picked), t(pos), t(neg), k).cpu().numpy()
+        np.testing.assert_array_equal(hits, R.topk_hits(users[picked], pos, neg, k))
+
+
+def test_topk_hits_edge_cases(gpu):
+    from lgcn_amd.recall import topk_hits
+
+    rng = np.random.default_rng(7)
+    users, pos, neg = _emb(rng, 10, 16), _emb(rng, 3, 16), _emb(rng, 2, 16)
+    t = lambda a: torch.from_numpy(a).to(gpu)
+    picked = np.arange(10)
+    # k == M: every positive is a hit
+    hits = topk_hits(t(users), torch.from_numpy(picked), t(pos), t(neg), 5).cpu().numpy()
+    np.testing.assert_array_equal(hits, np.full(10, 3))
+    with pytest.raises(RuntimeError, match="out of range"):
+        topk_hits(t(users), torch.from_numpy(picked), t(pos), t(neg), 6)
+    # no negatives at all
+    hits = topk_hits(t(users), torch.from_numpy(picked), t(pos), t(neg[:0]), 2).cpu().numpy()
+    np.testing.assert_array_equal(hits, np.full(10, 2))
+
+
+def test_compute_recall_at_k_matches_reference_golden(gpu):
+    """The reference's own compute_recall_at_k values (tests/golden/harness.npz, made by
+    importing reference utils/train_test.py), reproduced through the HIP path."""
+    from utils import train_test as TT
+
+    G = np.load(GOLDEN / "harness.npz")
+    embs = tuple(torch.from_numpy(a.copy()).to(gpu) for a in G["recall_embs"])
+    for k in (20, 100):
+        np.random.seed(7)
+        r = TT.compute_recall_at_k(embs, k=k)
+        assert r == pytest.approx(float(G[f"recall_k{k}"]), rel=1e-6, abs=0)
+
+
+def test_compute_recall_at_k_matches_oracle_at_scale(gpu):
+    from utils import train_test as TT
+
+    rng = np.random.default_rng(8)
+    d = 128
+    users, pos, neg = _emb(rng, 40000, d), _emb(rng, 40000, d), _emb(rng, 40000, d)
+    np.random.seed(3)
+    ref, detail = R.recall_at_k((users, pos, neg), k=100, return_detail=True)
+    np.random.seed(3)
+    got = TT.compute_recall_at_k(tuple(torch.from_numpy(a).to(gpu) for a in (users, pos, neg)), k=100)
+    if all((g > 1e-5).all() for _, _, g in detail):
+        assert got == pytest.approx(ref, rel=1e-6, abs=0)
+    else:
+        assert got == pytest.approx(ref, rel=1e-2)

@@ -1,0 +1,31 @@
+"""lgcn_legacy_choice (host C++) reproduces numpy's legacy np.random.choice(n, size,
+replace=False) — the reference's Recall@k user draw (utils/train_test.py:187) — pick for pick,
+and leaves the global generator in the state numpy itself would."""
+import numpy as np
+import pytest
+
+
+@pytest.mark.parametrize("n,size,draws", [(1, 1, 3), (2, 1, 5), (100, 100, 2), (1000, 17, 4), (621562, 100, 2),
+                                          (70001, 0, 2), (5, 3, 50)])
+def test_legacy_choice_matches_numpy(n, size, draws):
+    from lgcn_amd.recall import legacy_choice
+
+    for seed in (0, 7, 12345):
+        np.random.seed(seed)
+        np.random.random(seed % 5)  # start mid-block
+        got = legacy_choice(n, size, draws)
+        after = np.random.get_state()
+        np.random.seed(seed)
+        np.random.random(seed % 5)
+        want = np.stack([np.random.choice(n, size, replace=False) for _ in range(draws)])
+        ref_after = np.random.get_state()
+        np.testing.assert_array_equal(got, want)
+        assert after[2] == ref_after[2]
+        np.testing.assert_array_equal(after[1], ref_after[1])
+
+
+def test_legacy_choice_errors_like_numpy():
+    from lgcn_amd.recall import legacy_choice
+
+    with pytest.raises(ValueError):
+        legacy_choice(5, 6, 1)
