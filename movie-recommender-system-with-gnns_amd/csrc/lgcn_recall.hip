@@ -38,6 +38,11 @@ __device__ __forceinline__ uint32_t score_key(float s) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// inverse of score_key (the NaN key maps back to a NaN)
+__device__ __forceinline__ float key_score(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
+}
+
 // one 32-lane half-wave per row
 __global__ __launch_bounds__(kBlock) void k_normalize_rows(const float* __restrict__ x, const int64_t* __restrict__ idx,
                                                            int64_t rows, int64_t ld, int32_t d,
@@ -90,9 +95,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_filter(const float* __restr
     // to the per-query lists with ONE returning global atomic per query per flush
     __shared__ uint32_t st_key[4][kStage];
     __shared__ int32_t st_idx[4][kStage];
-    __shared__ uint32_t st_qr[4][kStage];  // query row | rank-within-query << 8
-    __shared__ int32_t st_qcnt[4][32];
-    __shared__ int32_t st_qbase[4][32];
+    __shared__ uint8_t st_row[4][kStage];  // query row within the wave's 32
+    __shared__ uint16_t st_rank[4][kStage];
+    __shared__ int32_t st_cnt[4][32];
+    __shared__ int32_t st_base[4][32];
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int i = lane & 31;
@@ -114,29 +120,34 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_filter(const float* __restr
             a[4 * v + 3] = t.w;
         }
     }
-    // this lane's 16 output rows: (r&3) + 8*(r>>2) + 4h; padding queries get a key no score
-    // reaches (their rows are zero, so their scores are 0, never NaN)
-    uint32_t th[16];
+    // this lane's 16 output rows: (r&3) + 8*(r>>2) + 4h. The test runs on floats, inclusively:
+    // !(score < t) keeps every score whose key is >= the threshold key (and NaN, which ranks
+    // first, and -0 beside +0 — extra entries are harmless, the selection works on exact keys).
+    // Padding queries get +inf (their zero rows score 0).
+    float th[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int64_t q = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        th[r] = (q < Qvalid) ? (thr ? thr[q] : 0u) : 0xFFFFFFFFu;
+        th[r] = (q < Qvalid) ? (thr ? key_score(thr[q]) : -__builtin_inff()) : __builtin_inff();
     }
-    if (lane < 32) st_qcnt[wv][lane] = 0;
     int scnt = 0;  // wave-uniform staged count
     const unsigned long long below = (1ull << lane) - 1ull;
-    auto flush = [&]() {  // wave-uniform
+    // flush (wave-uniform): ranks within each query row from LDS atomics (list order does not
+    // matter: selection ranks keys), one global atomic per row, then the stores
+    auto flush = [&]() {
+        if (lane < 32) st_cnt[wv][lane] = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int e = lane; e < scnt; e += 64)
+            st_rank[wv][e] = static_cast<uint16_t>(atomicAdd(&st_cnt[wv][st_row[wv][e]], 1));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane < 32) {
-            const int c = st_qcnt[wv][lane];
-            st_qbase[wv][lane] = c > 0 ? atomicAdd(list_n + q0 + lane, c) : 0;
-            st_qcnt[wv][lane] = 0;
+            const int c = st_cnt[wv][lane];
+            st_base[wv][lane] = c > 0 ? atomicAdd(list_n + q0 + lane, c) : 0;
         }
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         for (int e = lane; e < scnt; e += 64) {
-            const uint32_t qr = st_qr[wv][e];
-            const int row = static_cast<int>(qr & 255u);
-            const int32_t pos = st_qbase[wv][row] + static_cast<int32_t>(qr >> 8);
+            const int row = st_row[wv][e];
+            const int32_t pos = st_base[wv][row] + st_rank[wv][e];
             if (pos < cap) {
                 const int64_t q = q0 + row;
                 list_key[q * cap + pos] = st_key[wv][e];
@@ -179,14 +190,33 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_filter(const float* __restr
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
         const float* brow = &cs[buf][i * ROWF + h * H];
+        // B in groups of G float4 per LDS wait (G*4 MFMAs behind each wait)
+        constexpr int G = (H / 4) >= 4 ? 4 : (H / 4);
+#ifdef LGCN_VARIANT_NO_MFMA
+        for (int r = 0; r < 16; ++r) acc[r] = brow[r] * a[r];
+        if (false)
+#endif
 #pragma unroll
-        for (int v = 0; v < H / 4; ++v) {
-            const float4 bv = *reinterpret_cast<const float4*>(brow + 4 * v);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v], bv.x, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v + 1], bv.y, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v + 2], bv.z, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v + 3], bv.w, acc, 0, 0, 0);
+        for (int v0 = 0; v0 < H / 4; v0 += G) {
+            float4 bv[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) bv[g] = *reinterpret_cast<const float4*>(brow + 4 * (v0 + g));
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int v = v0 + g;
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v], bv[g].x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v + 1], bv[g].y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v + 2], bv[g].z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v + 3], bv[g].w, acc, 0, 0, 0);
+            }
         }
+#ifdef LGCN_VARIANT_NO_EPI
+        if (acc[0] == 12345.f && acc[15] == 54321.f) list_n[0] = 1;  // keep acc live; never true
+        if (nxt < nblk) land(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+        continue;
+#endif
         // epilogue: column = candidate j (this lane's), rows = queries; branch-free test, and
         // a wave-uniform branch only for the (rare) slots where some lane passes
         const int64_t j = cb * 32 + i;
@@ -196,9 +226,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_filter(const float* __restr
         for (int r = 0; r < 16; ++r) {
             const int row0 = (r & 3) + 8 * (r >> 2);
             const int row = row0 + 4 * h;
-            const uint32_t key = score_key(acc[r]);
-            const bool take = jok & (key >= th[r]);
+            const bool take = jok & !(acc[r] < th[r]);
             if (thr == nullptr) {  // dense mode: every subset score at its subset slot
+                const uint32_t key = score_key(acc[r]);
                 if (take) {
                     const int64_t q = q0 + row;
                     list_key[q * cap + j] = key;
@@ -210,19 +240,11 @@ __global__ __launch_bounds__(kBlock, 2) void k_score_filter(const float* __restr
             if (m == 0ull) continue;
             const int n = __popcll(m);
             if (scnt + n > kStage) flush();
-            const unsigned lo = static_cast<unsigned>(m), hi = static_cast<unsigned>(m >> 32);
-            const int c0 = st_qcnt[wv][row0], c1 = st_qcnt[wv][row0 + 4];
             if (take) {
                 const int sl = scnt + __popcll(m & below);
-                const unsigned half = h ? hi : lo;
-                const int rank = (h ? c1 : c0) + __popc(half & static_cast<unsigned>(below >> (32 * h)));
-                st_key[wv][sl] = key;
+                st_key[wv][sl] = score_key(acc[r]);
                 st_idx[wv][sl] = jj;
-                st_qr[wv][sl] = static_cast<uint32_t>(row) | (static_cast<uint32_t>(rank) << 8);
-            }
-            if (lane == 0) {
-                st_qcnt[wv][row0] = c0 + __popc(lo);
-                st_qcnt[wv][row0 + 4] = c1 + __popc(hi);
+                st_row[wv][sl] = static_cast<uint8_t>(row);
             }
             scnt += n;
         }

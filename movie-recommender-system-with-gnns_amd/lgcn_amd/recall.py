@@ -92,7 +92,7 @@ def topk_hits(users: torch.Tensor, picked: torch.Tensor, pos: torch.Tensor, neg:
         _ffi.check(lib.lgcn_score_filter(ws.Qn.data_ptr(), Qpad, Q, ws.Cn.data_ptr(), M, 1, D, ws.thr.data_ptr(),
                                          ws.lkey.data_ptr(), ws.lidx.data_ptr(), ws.lcnt.data_ptr(), cap, s),
                    "lgcn_score_filter")
-        if int(ws.lcnt.max().item()) <= cap:
+        if int(ws.lcnt[:Q].max().item()) <= cap:
             _ffi.check(lib.lgcn_select_topk(ws.lkey.data_ptr(), ws.lidx.data_ptr(), ws.lcnt.data_ptr(), 0, cap, k,
                                             P, Qpad, Q, None, ws.hits.data_ptr(), s), "lgcn_select_topk")
             return ws.hits[:Q].clone()
