@@ -12,9 +12,10 @@ sharding of independent units, no data-path collective (scaling: weak). The barr
 max-over-ranks time go over RCCL.
 
 Also reported (one JSON line on rank 0):
-  roofline     — achieved algorithmic GB/s of the dominant kernel (the item pass of lgcn_spmm),
-                 timed live with HIP events on its launching stream, vs the 8 TB/s HBM peak;
-                 bytes per launch = E*(4d+8) + N*(4d+8).
+  roofline     — achieved algorithmic GB/s of the dominant kernel (the item pass, k_spmm_vec;
+                 at C2 one launch per source slice, lgcn_amd.sliced), timed live with HIP events
+                 on its launching stream, vs the 8 TB/s HBM peak; bytes per layer =
+                 E*(4d+8) + N*(4d+8), per launch = that / launches per layer.
   cpu_baseline — the reference's CPU op sequence (PyG 2.4.0 LGConv restated with torch CPU
                  primitives, oracle/lgconv_torch.py) on a bounded sample, rank 0, N=1 only.
 """
@@ -207,9 +208,16 @@ def main():
     t0 = time.perf_counter()
     # side_split = U: rows gathering the item table run first, then rows gathering the user table
     plan = PropagationPlan(ei, N, args.chunk or DEFAULT_CHUNK, side_split=U)
+    # the schedule the forward runs at this width: source-sliced (one lgcn_spmm_run launch per
+    # slice per layer) when lgcn_amd.plan.slice_bytes_for enables it, else the plain item list
+    from lgcn_amd.sliced import SlicedDirection
+
+    sched = plan.schedule("fwd", d)
+    n_slices = sum(1 for _, n in sched.launches if n) if isinstance(sched, SlicedDirection) else 1
     torch.cuda.synchronize()
     log(f"[rank {rank}] plan: {plan.fwd.n_items} items, {plan.fwd.n_splits} split rows, "
-        f"{plan.fwd.n_partials} partials, {plan.nbytes() / 1e6:.0f} MB ({time.perf_counter() - t0:.2f} s)")
+        f"{plan.fwd.n_partials} partials, {plan.nbytes() / 1e6:.0f} MB; "
+        f"{n_slices} source slice(s) per layer, {sched.n_splits} chunked rows ({time.perf_counter() - t0:.2f} s)")
 
     def step():
         return lgcn_amd.propagate_forward(user_w, item_w, plan, K)
@@ -233,7 +241,8 @@ def main():
         timer.active = False
         lgcn_amd.set_launch_timer(None)
 
-    kernel_ms = timer.mean_ms()
+    # the timer brackets each layer's item pass: n_slices launches (+ the short gaps between them)
+    kernel_ms = timer.mean_ms() / n_slices
     edges_total = E
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -249,7 +258,9 @@ def main():
     if c5:
         edges_total = E  # feature-sharded: the ranks together propagate one graph
     value = K * edges_total * args.steps / elapsed
-    bytes_per_launch = E * (4 * d + 8) + N * (4 * d + 8)
+    # algorithmic bytes of one layer, spread over the layer's n_slices launches
+    bytes_per_layer = E * (4 * d + 8) + N * (4 * d + 8)
+    bytes_per_launch = bytes_per_layer / n_slices
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     if c5:
         workload = f"C5_synthetic_10Mx1M_5e8_K{K}_d{d_full}" + ("" if args.scale == 1.0 else f"_scale{args.scale}")
@@ -277,8 +288,11 @@ def main():
                                   f"{world} independent graph instance(s), one per GPU, no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": f"k_spmm_vec<{kernel_lpr(d)}> (lgcn_spmm_items)", "kernel_ms": kernel_ms,
-                     "bytes_per_launch": bytes_per_launch},
+                     "kernel": (f"k_spmm_vec<{kernel_lpr(d)},sliced> (lgcn_spmm_run, {n_slices} source-slice "
+                                f"launches per layer)" if n_slices > 1 else
+                                f"k_spmm_vec<{kernel_lpr(d)}> (lgcn_spmm_items)"),
+                     "kernel_ms": kernel_ms, "bytes_per_launch": bytes_per_launch,
+                     "launches_per_layer": n_slices},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not c5:

@@ -175,6 +175,17 @@ int lgcn_spmm_combine(const lgcn_item_t* items, int64_t n_items,
                       float* acc_lo, float* acc_hi, int64_t acc_split,
                       float* partial, int32_t mode, float div, float mul,
                       lgcn_stream_t stream);
+/* One launch of a source-sliced schedule (the item pass only). Row items carry flags in the high
+ * bits of len: 0x20000000 = the row's FIRST segment (its sum starts at 0, else it continues from
+ * run[row]), 0x40000000 = its LAST segment (the epilogue runs, else the running sum is stored to
+ * run[row], [N, d]); the low 29 bits are the length. Partial-slot items (dst < 0) carry no flags.
+ * Issued once per slice in ascending source order, each row's sum stays one sequential chain in
+ * CSR order; lgcn_spmm_combine afterwards finishes the chunked (hub) rows. */
+int lgcn_spmm_run(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* splits, int64_t n_splits,
+                  const int32_t* col, const float* val, int64_t N, int32_t d, const float* x_lo, const float* x_hi,
+                  int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split, float* y, float* acc_lo,
+                  float* acc_hi, int64_t acc_split, float* partial, int32_t mode, float div, float mul,
+                  lgcn_stream_t stream, float* run);
 
 /* out[i] = (in[i] * mul) / div over n floats: the gradient that MulBackward (× 1/(K+1))
  * then MeanBackward (÷ (K+1)) hand to every layer output (reference models/light_gcn.py:36). */

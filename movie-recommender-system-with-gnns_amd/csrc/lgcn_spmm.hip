@@ -51,7 +51,13 @@ struct SpmmArgs {
     int32_t mode;
     float div;
     float mul;
+    float* run;  // sliced launches: running row sums between a row's source-slice segments
 };
+
+// Sliced-schedule item flags, in the high bits of lgcn_item_t::len (rows, not partial chunks).
+constexpr int32_t kItemFirst = 0x20000000;
+constexpr int32_t kItemLast = 0x40000000;
+constexpr int32_t kItemLenMask = 0x1FFFFFFF;
 
 template <class T>
 __device__ __forceinline__ T* split_row(T* lo, T* hi, int64_t split, int64_t r, int64_t stride) {
@@ -109,20 +115,34 @@ __device__ __forceinline__ void finish_row_vec(const SpmmArgs& a, int64_t r, int
 // the lanes load (col, val) coalesced — the NEXT batch's pair is loaded before the current
 // batch's gathers are issued, so that latency overlaps them — then UNROLL neighbour rows are
 // gathered (one float4 per lane each) before the first add, and added in CSR order.
-template <int LPR, int NV, int UNROLL>
+// SLICED: one launch of a source-sliced schedule (lgcn_spmm_run). A row item continues the row's
+// running sum from a.run unless it is the row's FIRST segment, and runs the epilogue only on its
+// LAST one; the sum stays one sequential chain in CSR order across launches.
+template <int LPR, int NV, int UNROLL, bool SLICED = false>
 __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
     constexpr int GPB = kBlock / LPR;
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
     const int64_t item = int64_t(blockIdx.x) * GPB + g;
     if (item >= a.n_items) return;
-    const lgcn_item_t it = a.items[item];
+    lgcn_item_t it = a.items[item];
+    int32_t flags = kItemFirst | kItemLast;
+    if (SLICED && it.dst >= 0) {
+        flags = it.len & (kItemFirst | kItemLast);
+        it.len &= kItemLenMask;
+    }
     const int64_t d4 = int64_t(LPR) * NV;
     const float4* __restrict__ xlo = reinterpret_cast<const float4*>(a.x_lo) + l;
     const float4* __restrict__ xhi = reinterpret_cast<const float4*>(a.x_hi) + l;
     float4 acc[NV];
+    if (SLICED && !(flags & kItemFirst)) {
+        const float4* r = reinterpret_cast<const float4*>(a.run) + int64_t(it.dst) * d4 + l;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < NV; ++k) acc[k] = r[k * LPR];
+    } else {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     int cn = 0;
     float wn = 0.f;
     if (l < it.len) {
@@ -166,6 +186,12 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
         float4* p = reinterpret_cast<float4*>(a.partial) + int64_t(-it.dst - 1) * d4 + l;
 #pragma unroll
         for (int k = 0; k < NV; ++k) p[k * LPR] = acc[k];
+        return;
+    }
+    if (SLICED && !(flags & kItemLast)) {
+        float4* r = reinterpret_cast<float4*>(a.run) + int64_t(it.dst) * d4 + l;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) r[k * LPR] = acc[k];
         return;
     }
     finish_row_vec<LPR, NV>(a, it.dst, l, acc);
@@ -294,7 +320,10 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass) {
     constexpr int GPB = kBlock / LPR;
     if ((pass & PASS_ITEMS) && a.n_items > 0) {
         const int64_t blocks = (a.n_items + GPB - 1) / GPB;
-        k_spmm_vec<LPR, NV, UNROLL><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+        if (a.run != nullptr)
+            k_spmm_vec<LPR, NV, UNROLL, true><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+        else
+            k_spmm_vec<LPR, NV, UNROLL><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
         if (int rc = check_launch("k_spmm_vec")) return rc;
     }
     if ((pass & PASS_COMBINE) && a.n_splits > 0) {
@@ -349,13 +378,13 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
               const int32_t* col, const float* val, int64_t N, int32_t d, const float* x_lo,
               const float* x_hi, int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split,
               float* y, float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
-              float div, float mul, lgcn_stream_t stream, int pass) {
+              float div, float mul, lgcn_stream_t stream, int pass, float* run = nullptr) {
     if (N < 0 || d <= 0 || n_items < 0 || n_splits < 0)
         return fail(LGCN_E_ARG, "lgcn_spmm: bad sizes (N=%lld d=%d)", (long long)N, d);
     if (mode < LGCN_EPI_INIT || mode > LGCN_EPI_SCALE) return fail(LGCN_E_ARG, "lgcn_spmm: bad mode %d", mode);
-    if (N == 0 || n_items == 0) return LGCN_OK;
+    if (N == 0 || (n_items == 0 && n_splits == 0)) return LGCN_OK;
     // col/val may be NULL for an edge-free plan (every item then has len 0)
-    if (!items || !x_lo || !acc_lo) return fail(LGCN_E_ARG, "lgcn_spmm: null items/x/acc");
+    if ((n_items > 0 && !items) || !x_lo || !acc_lo) return fail(LGCN_E_ARG, "lgcn_spmm: null items/x/acc");
     if (x_split < N && !x_hi) return fail(LGCN_E_ARG, "lgcn_spmm: x_hi required (x_split < N)");
     if (acc_split < N && !acc_hi) return fail(LGCN_E_ARG, "lgcn_spmm: acc_hi required (acc_split < N)");
     const bool needs_e = (mode == LGCN_EPI_INIT || mode == LGCN_EPI_FINAL_E);
@@ -366,7 +395,7 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
         return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm: d=%d unsupported (d > %d needs d %% 4 == 0)", d, 64 * KMAX);
 
     SpmmArgs a{items, n_items, splits, n_splits, col, val, x_lo, x_hi, x_split, e_lo, e_hi, e_split,
-               y, acc_lo, acc_hi, acc_split, partial, d, mode, div, mul};
+               y, acc_lo, acc_hi, acc_split, partial, d, mode, div, mul, run};
     hipStream_t s = as_stream(stream);
 
     bool vec_ok = (d % 4 == 0) && aligned16(x_lo) && aligned16(acc_lo) && aligned16(partial) &&
@@ -389,6 +418,7 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
             default: break;
         }
     }
+    if (run != nullptr) return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm_run: needs d in {4,8,...,1024} and aligned rows");
     if (d > 64 * KMAX) return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm: d=%d unsupported", d);
     return launch_scalar(a, s, pass);
 }
@@ -410,6 +440,10 @@ extern "C" {
 int lgcn_spmm(LGCN_SPMM_PARAMS) { return spmm_impl(LGCN_SPMM_ARGS, PASS_BOTH); }
 int lgcn_spmm_items(LGCN_SPMM_PARAMS) { return spmm_impl(LGCN_SPMM_ARGS, PASS_ITEMS); }
 int lgcn_spmm_combine(LGCN_SPMM_PARAMS) { return spmm_impl(LGCN_SPMM_ARGS, PASS_COMBINE); }
+int lgcn_spmm_run(LGCN_SPMM_PARAMS, float* run) {
+    if (!run) return fail(LGCN_E_ARG, "lgcn_spmm_run: null running-sum buffer");
+    return spmm_impl(LGCN_SPMM_ARGS, PASS_ITEMS, run);
+}
 
 int lgcn_scale(const float* in, float* out, int64_t n, float mul, float div, lgcn_stream_t stream) {
     if (n < 0 || (n > 0 && (!in || !out))) return fail(LGCN_E_ARG, "lgcn_scale: bad args");

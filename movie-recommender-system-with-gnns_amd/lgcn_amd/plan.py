@@ -15,6 +15,7 @@ edge order inside a row, which is the order CPU scatter_add_/index_add_ add in.
 from __future__ import annotations
 
 import dataclasses
+import os
 import weakref
 
 import torch
@@ -22,6 +23,22 @@ import torch
 from . import _ffi
 
 DEFAULT_CHUNK = 256
+
+
+def slice_bytes_for(num_nodes: int, d: int) -> int:
+    """Source-slice size for a full-graph propagation of width d (0 = no slicing). Measured on
+    the C2 graph (tools/sliced_probe.py, profiles/r01g_sliced): slicing pays while the gathered
+    table is small enough that re-reading the running row sums once per slice costs less than the
+    cache misses it saves — about 8 slices of 8–24 MB for tables of 16–512 MB; beyond that (C5:
+    11 GB) the plain schedule is faster. LGCN_SLICE_MB overrides (0 disables)."""
+    env = os.environ.get("LGCN_SLICE_MB")
+    if env is not None:
+        v = float(env)
+        return int(v * 2**20) if v > 0 else 0
+    x = int(num_nodes) * int(d) * 4
+    if x < 16 * 2**20 or x > 512 * 2**20:
+        return 0
+    return int(min(max(x // 8, 8 * 2**20), 24 * 2**20))
 
 
 @dataclasses.dataclass
@@ -167,6 +184,25 @@ class PropagationPlan:
         if bad:
             raise IndexError(f"edge_index holds {bad} edge(s) with a node id outside [0, {self.num_nodes})")
         self._bwd: CsrDirection | None = None
+        self._sched: dict = {}
+
+    def schedule(self, which: str, d: int):
+        """The direction ('fwd' or 'bwd') to propagate rows of width d with: the source-sliced
+        schedule (lgcn_amd.sliced) when slice_bytes_for(N, d) enables it for this plan, else the
+        plain CsrDirection. Built once per (direction, d)."""
+        key = (which, int(d))
+        if key in self._sched:
+            return self._sched[key]
+        direction = self.fwd if which == "fwd" else self.bwd
+        out = direction
+        sb = 0 if self.touched is not None else slice_bytes_for(self.num_nodes, d)
+        if sb and self.num_edges:
+            from .sliced import build_sliced, slice_bounds
+
+            out = build_sliced(direction, self.num_nodes, slice_bounds(self.num_nodes, self.side_split, d, sb),
+                               direction.chunk) or direction
+        self._sched[key] = out
+        return out
 
     @property
     def bwd(self) -> CsrDirection:

@@ -16,6 +16,7 @@ import torch
 
 from . import _ffi
 from .plan import CsrDirection, PropagationPlan
+from .sliced import SlicedDirection, spmm_sliced, spmm_sliced_combine
 
 # Optional per-launch timing hook (bench.py): a callable(name) -> context manager that records
 # HIP events around the main propagation kernel on the launching stream.
@@ -31,15 +32,28 @@ def _f32(x: float) -> float:
     return float(np.float32(x))
 
 
-def spmm(direction: CsrDirection, N: int, d: int, x, e, acc, y, mode: int, div: float = 1.0, mul: float = 1.0,
+def spmm(direction, N: int, d: int, x, e, acc, y, mode: int, div: float = 1.0, mul: float = 1.0,
          partial: torch.Tensor | None = None, stream: int | None = None) -> None:
-    """One lgcn_spmm call. x / e / acc are split tables: (lo, hi, split) with hi=None for a
-    single [N, d] table (split = N)."""
+    """One layer: one lgcn_spmm call over a CsrDirection, or the per-slice lgcn_spmm_run launches
+    (+ hub combine) over a SlicedDirection. x / e / acc are split tables: (lo, hi, split) with
+    hi=None for a single [N, d] table (split = N)."""
     lib = _ffi.load()
     if stream is None:
         stream = _ffi.stream_of(acc[0].device)
     if direction.n_partials > 0 and partial is None:
         partial = torch.empty((direction.n_partials, d), dtype=torch.float32, device=acc[0].device)
+    if isinstance(direction, SlicedDirection):
+        # the layer output doubles as the running-sum buffer (a row's y is final only after its
+        # last item); the final-layer modes have no y, so they get a scratch one
+        run = y if y is not None else torch.empty((N, d), dtype=torch.float32, device=acc[0].device)
+        if _launch_timer is not None:
+            # one bracket around the layer's slice launches (2 events per layer, not per launch)
+            with _launch_timer(d):
+                spmm_sliced(direction, N, d, x, e, acc, y, mode, div, mul, run, partial, stream, combine=False)
+            spmm_sliced_combine(direction, N, d, x, e, acc, y, mode, div, mul, partial, stream)
+        else:
+            spmm_sliced(direction, N, d, x, e, acc, y, mode, div, mul, run, partial, stream)
+        return
     xl, xh, xs = x
     el, eh, es = e if e is not None else (None, None, N)
     al, ah, as_ = acc
@@ -92,7 +106,7 @@ def propagate_forward(user_w: torch.Tensor, item_w: torch.Tensor, plan: Propagat
         _ffi.check(lib.lgcn_copy_scale(user_w.data_ptr(), item_w.data_ptr(), U, N, d, out.data_ptr(), div, mul, stream),
                    "lgcn_copy_scale")
         return out
-    f = plan.fwd
+    f = plan.schedule("fwd", d)
     partial = torch.empty((f.n_partials, d), dtype=torch.float32, device=dev) if f.n_partials else None
     if K == 1:
         spmm(f, N, d, x0, x0, acc, None, _ffi.EPI_FINAL_E, div, mul, partial, stream)
@@ -129,7 +143,7 @@ def propagate_backward(dout: torch.Tensor, plan: PropagationPlan, U: int, K: int
         return grad_user, grad_item
     g = torch.empty((N, d), dtype=torch.float32, device=dev)
     _ffi.check(lib.lgcn_scale(dout.data_ptr(), g.data_ptr(), N * d, mul, div, stream), "lgcn_scale")
-    b = plan.bwd
+    b = plan.schedule("bwd", d)
     partial = torch.empty((b.n_partials, d), dtype=torch.float32, device=dev) if b.n_partials else None
     cur = g
     bufs = [torch.empty((N, d), dtype=torch.float32, device=dev) for _ in range(min(2, K - 1))]
@@ -158,7 +172,7 @@ def propagate_backward_seeded(grad_user: torch.Tensor, grad_item: torch.Tensor, 
         return
     dev = grad_user.device
     stream = _ffi.stream_of(dev)
-    b = plan.bwd
+    b = plan.schedule("bwd", d)
     partial = torch.empty((b.n_partials, d), dtype=torch.float32, device=dev) if b.n_partials else None
     g = (grad_user, grad_item, U)
     if K == 1:
@@ -207,7 +221,7 @@ def lgconv_forward(x: torch.Tensor, plan: PropagationPlan) -> torch.Tensor:
     if N != plan.num_nodes:
         raise ValueError(f"x has {N} rows, plan has {plan.num_nodes} nodes")
     out = torch.empty_like(x)
-    spmm(plan.fwd, N, d, (x, None, N), None, (out, None, N), None, _ffi.EPI_STORE)
+    spmm(plan.schedule("fwd", d), N, d, (x, None, N), None, (out, None, N), None, _ffi.EPI_STORE)
     return out
 
 
@@ -215,7 +229,7 @@ def lgconv_backward(dy: torch.Tensor, plan: PropagationPlan) -> torch.Tensor:
     dy = dy.contiguous().float()
     N, d = dy.shape
     dx = torch.empty_like(dy)
-    spmm(plan.bwd, N, d, (dy, None, N), None, (dx, None, N), None, _ffi.EPI_STORE)
+    spmm(plan.schedule("bwd", d), N, d, (dy, None, N), None, (dx, None, N), None, _ffi.EPI_STORE)
     return dx
 
 

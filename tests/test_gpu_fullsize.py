@@ -39,7 +39,8 @@ def test_c2_full_forward_matches_oracle(gpu, c2):
 
 
 def test_c2_single_layer_bitwise_on_unsplit_rows(gpu, c2):
-    """One layer: every row that is one schedule item (not cut into chunks) is bitwise the
+    """One layer: every row summed as one sequential chain (not cut into chunks — with the
+    source-sliced schedule, a chain that runs through several slice launches) is bitwise the
     reference CPU scatter_add_ result; split (hub) rows — up to 62k terms each — are within 1e-5
     relative and at least as close to the exact float64 sum as the sequential CPU order."""
     from lgcn_amd.propagate import lgconv_forward
@@ -49,7 +50,8 @@ def test_c2_single_layer_bitwise_on_unsplit_rows(gpu, c2):
     y = lgconv_forward(torch.from_numpy(x).to(gpu), plan).cpu().numpy()
     _, w = c_oracle.gcn_norm(g.edge_index, g.num_nodes)
     ref = c_oracle.lgconv(x, g.edge_index, w)
-    split_rows = plan.fwd.splits[: plan.fwd.n_splits, 0].cpu().numpy()
+    sched = plan.schedule("fwd", 64)  # the source-sliced schedule at this size (lgcn_amd.sliced)
+    split_rows = sched.splits[: sched.n_splits, 0].cpu().numpy()
     mask = np.ones(g.num_nodes, bool)
     mask[split_rows] = False
     assert mask.sum() > 0.9 * g.num_nodes

@@ -1,0 +1,56 @@
+"""Turn a round profile (tools/profile_round.sh output dir) into the roofline.traffic entry of
+profiles/pmc_traffic.json: average memory-side bytes per k_spmm_vec launch =
+FETCH_SIZE x calibration (tools/calib_fetch.py: a permutation gather that must read every byte
+once) + WRITE_SIZE, each from its own --pmc pass.
+python tools/pmc_to_traffic.py <profile dir> <workload key> [--kernel k_spmm_vec]"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_launch(path, counter, kernel):
+    vals = {}
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof")
+    ap.add_argument("workload")
+    ap.add_argument("--kernel", default="k_spmm_vec")
+    args = ap.parse_args()
+    # FETCH_SIZE / WRITE_SIZE are in KiB on gfx950 (rocprofv3 derived counters)
+    fetch = per_launch(os.path.join(args.prof, "pmc_fetch"), "FETCH_SIZE", args.kernel)
+    write = per_launch(os.path.join(args.prof, "pmc_write"), "WRITE_SIZE", args.kernel)
+    cal_f = per_launch(os.path.join(args.prof, "calib_fetch"), "FETCH_SIZE", "k_spmm_vec")
+    tj = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    data = json.load(open(tj))
+    factor = data[next(iter(data))].get("fetch_correction_factor")
+    log = os.path.join(args.prof, "calib_fetch.log")
+    if cal_f and os.path.exists(log):
+        for line in open(log):
+            if line.startswith("expected_read_bytes"):
+                factor = float(line.split()[1]) / (statistics.median(cal_f) * 1024)
+    f = statistics.mean(fetch) * 1024 * factor
+    w = statistics.mean(write) * 1024
+    data[args.workload] = {
+        "hbm_bytes_per_launch": f + w, "fetch_bytes_corrected": f, "write_bytes": w,
+        "fetch_correction_factor": factor, "kernel": args.kernel, "launches_measured": len(fetch),
+        "source": f"{os.path.relpath(args.prof, ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
+        "note": "average memory-side (L2-miss) bytes per launch; FETCH_SIZE also counts Infinity-Cache hits, so "
+                "this bounds HBM traffic from above"}
+    json.dump(data, open(tj, "w"), indent=1)
+    print(json.dumps(data[args.workload], indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,95 @@
+"""Probe: source-sliced forward (lgcn_amd.sliced) vs the default schedule on the C2 graph.
+python tools/sliced_probe.py [--mb 1.5,2.5,4,8]"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "movie-recommender-system-with-gnns_amd"))
+
+import lgcn_amd  # noqa: E402
+from lgcn_amd import synth  # noqa: E402
+from lgcn_amd.plan import PropagationPlan  # noqa: E402
+from lgcn_amd.sliced import build_sliced, propagate_forward_sliced, slice_bounds  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mb", default="1.5,2.5,4,8")
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--c5", type=float, default=0.0, help="use the C5 generator at this scale (0 = C2 graph)")
+    ap.add_argument("--layers", type=int, default=3)
+    ap.add_argument("--no-check", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    if args.c5:
+        U, I = int(synth.C5_USERS * args.c5), int(synth.C5_ITEMS * args.c5)
+        ei = synth.bipartite_device(U, I, int(synth.C5_PAIRS * args.c5), seed=0, device=dev)
+        N, E = U + I, int(ei.shape[1])
+    else:
+        g = synth.ml25m_shaped(seed=0)
+        U, I, N, E = g.num_users, g.num_items, g.num_nodes, g.num_edges
+        ei = torch.from_numpy(g.edge_index).to(dev)
+    K, d = args.layers, args.dim
+    gen = torch.Generator(device=dev).manual_seed(0)
+    uw = torch.randn(U, d, device=dev, generator=gen) * 0.01
+    iw = torch.randn(I, d, device=dev, generator=gen) * 0.01
+    plan = PropagationPlan(ei, N, 256, side_split=U)
+    deg = (plan.fwd.rowptr[1:] - plan.fwd.rowptr[:-1])
+
+    def bench(fn):
+        with torch.no_grad():
+            for _ in range(3):
+                out = fn()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(args.steps):
+                out = fn()
+            torch.cuda.synchronize()
+        return out, (time.perf_counter() - t) / args.steps * 1e3
+
+    ref, ms0 = bench(lambda: lgcn_amd.propagate_forward(uw, iw, plan, K))
+    print(f"default      {ms0:.3f} ms/step  {K * E / ms0 / 1e6:.2f} e9 edges/s (E={E}, N={N}, d={d})", flush=True)
+    for mb in [float(v) for v in args.mb.split(",")]:
+        b = slice_bounds(N, U, d, int(mb * 2**20))
+        t0 = time.perf_counter()
+        sd = build_sliced(plan.fwd, N, b, 256)
+        torch.cuda.synchronize()
+        tb = time.perf_counter() - t0
+        out, ms = bench(lambda: propagate_forward_sliced(uw, iw, sd, K))
+        hub = torch.zeros(N, dtype=torch.bool, device=dev)
+        if sd.n_splits:
+            hub[sd.splits[:, 0].long()] = True
+        # rows summed sequentially by both schedules (K=3: only when their whole 2-hop is too —
+        # so compare the layer-exact subset loosely and report the max row-relative difference)
+        rel = ((out - ref).abs().max(1).values / ref.abs().max(1).values.clamp_min(1e-30))
+        print(f"slices {mb:4.1f} MB: {len(b) - 1:3d} launches/layer, {sd.n_splits} hub rows, build {tb:.2f} s: "
+              f"{ms:.3f} ms/step  {K * E / ms / 1e6:.2f} e9 edges/s  max row-rel diff {rel.max().item():.2e}",
+              flush=True)
+    if args.no_check:
+        return
+    # single layer bitwise check on rows unsplit in both schedules
+    from lgcn_amd.sliced import spmm_sliced
+    from lgcn_amd import _ffi
+    sd = build_sliced(plan.fwd, N, slice_bounds(N, U, d, int(2.5 * 2**20)), 256)
+    s = _ffi.stream_of(dev)
+    o1 = torch.empty((N, d), device=dev)
+    o2 = torch.empty((N, d), device=dev)
+    lgcn_amd.propagate.spmm(plan.fwd, N, d, (uw, iw, U), None, (o1, None, N), None, _ffi.EPI_STORE, stream=s)
+    run = torch.empty((N, d), device=dev)
+    part = torch.empty((max(sd.n_partials, 1), d), device=dev)
+    spmm_sliced(sd, N, d, (uw, iw, U), None, (o2, None, N), None, _ffi.EPI_STORE, 1.0, 1.0, run, part, s)
+    hub = torch.zeros(N, dtype=torch.bool, device=dev)
+    if sd.n_splits:
+        hub[sd.splits[:, 0].long()] = True
+    ok = (deg <= 256) & ~hub
+    eq = torch.equal(o1[ok], o2[ok])
+    print(f"one layer: bitwise equal on {int(ok.sum())} rows unsplit in both: {eq}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
