@@ -30,7 +30,8 @@ def slice_bytes_for(num_nodes: int, d: int) -> int:
     the C2 graph (tools/sliced_probe.py, profiles/r01g_sliced): slicing pays while the gathered
     table is small enough that re-reading the running row sums once per slice costs less than the
     cache misses it saves — about 8 slices of 8–24 MB for tables of 16–512 MB; beyond that (C5:
-    11 GB) the plain schedule is faster. LGCN_SLICE_MB overrides (0 disables)."""
+    11 GB) the plain schedule is faster. PropagationPlan.schedule also requires >= 8 edges per
+    row per slice. LGCN_SLICE_MB overrides the size and that density test (0 disables)."""
     env = os.environ.get("LGCN_SLICE_MB")
     if env is not None:
         v = float(env)
@@ -199,8 +200,12 @@ class PropagationPlan:
         if sb and self.num_edges:
             from .sliced import build_sliced, slice_bounds
 
-            out = build_sliced(direction, self.num_nodes, slice_bounds(self.num_nodes, self.side_split, d, sb),
-                               direction.chunk) or direction
+            bounds = slice_bounds(self.num_nodes, self.side_split, d, sb)
+            # the running sums cost ~2 row passes per slice: worth it only for dense enough graphs
+            # (C2: 112 edges per row; a 5 % validation edge set, ~6, is faster unsliced)
+            forced = os.environ.get("LGCN_SLICE_MB") is not None
+            if forced or self.num_edges >= 8 * (len(bounds) - 1) * self.num_nodes:
+                out = build_sliced(direction, self.num_nodes, bounds, direction.chunk) or direction
         self._sched[key] = out
         return out
 
