@@ -151,6 +151,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for runs; gloo to rehearse N ranks on one GPU")
     ap.add_argument("--torch-adam", action="store_true", help="train: torch Adam + clip_grad_norm_ (reference ops)")
     ap.add_argument("--no-graphs", action="store_true", help="train: run the fused step eagerly (no hipGraph replay)")
+    ap.add_argument("--dense-adam", action="store_true",
+                    help="train: dense FusedAdam over all rows every step instead of the row-lazy exact Adam")
     ap.add_argument("--autograd", action="store_true",
                     help="train: reference-style step (compute_embeddings + bpr_loss + autograd) instead of "
                          "the fused no-autograd step")
@@ -351,8 +353,14 @@ def run_train(args):
         f"({time.perf_counter() - t0:.1f} s)")
     torch.manual_seed(0)
     model = LightGCN(U, I, num_layers=K, dim_h=d).to(dev)
+    lazy = not (args.autograd or args.torch_adam or args.dense_adam) and world == 1
     if args.torch_adam:
         opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    elif lazy:
+        from lgcn_amd.optim import RowLazyAdam
+
+        opt = RowLazyAdam(model.user_embedding.weight.data, model.item_embedding.weight.data, lr=1e-3,
+                          max_grad_norm=1)
     else:
         from lgcn_amd.optim import FusedAdam
 
@@ -365,7 +373,8 @@ def run_train(args):
     if not args.autograd:
         from lgcn_amd.train_step import FusedTrainStep
 
-        fused = FusedTrainStep(model, opt, world=world, graphs=not args.no_graphs and not args.torch_adam)
+        fused = FusedTrainStep(model, opt, world=world, graphs=not args.no_graphs and not args.torch_adam,
+                               lazy=lazy)
 
     def step(bidx):
         batch = batches[bidx]
@@ -384,6 +393,8 @@ def run_train(args):
     share = D.rank_share(len(batches), world, rank, seed=0, epoch=0)
     for i in range(max(args.warmup, 2 * len(share))):  # warm-up builds every batch's plan
         step(share[i % len(share)])
+        if fused is not None and (i + 1) % len(share) == 0:
+            fused.sync()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -391,6 +402,10 @@ def run_train(args):
     edges = 0
     for i in range(args.steps):
         edges += step(share[i % len(share)])
+        # row-lazy Adam: parameters are made current once per epoch (as evaluation needs them),
+        # inside the timed region
+        if fused is not None and ((i + 1) % len(share) == 0 or i + 1 == args.steps):
+            fused.sync()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -410,7 +425,9 @@ def run_train(args):
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (seeded ML-25M-shaped graph, 90/5/5 directed split)",
         "config": {"workload": f"C{3 if world == 1 else 4}_cluster_gcn_train", "parts": args.parts,
-                   "optimizer": "torch Adam + clip_grad_norm_" if args.torch_adam else "lgcn FusedAdam (clip fused)",
+                   "optimizer": ("torch Adam + clip_grad_norm_" if args.torch_adam else
+                                 "lgcn RowLazyAdam (exact row-lazy Adam + clip, flushed each epoch)" if lazy else
+                                 "lgcn FusedAdam (clip fused)"),
                    "step": "autograd (reference ops)" if args.autograd else
                            ("fused sparse step" + ("" if (args.no_graphs or args.torch_adam) else ", hipGraph per batch")),
                    "parts_per_batch": q, "f_intra": f_intra, "layers": K, "dim": d, "num_users": U,

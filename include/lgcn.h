@@ -230,13 +230,42 @@ int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C
  * Optional second source C2 (nullable): the same per-row sums of C2 are parked in c2buf[b_first]
  * (c2flag[b_first] = 1; the launch clears c2flag) for lgcn_flagged_rows_add to add LATER (the
  * negatives' reg-gradient rows must land after the backward). *overflow (nullable, caller-zeroed)
- * is set if a workgroup's list overflowed — parked sums would then be split; callers check it. */
+ * is set if a workgroup's list overflowed — parked sums would then be split; callers check it.
+ * store_unless (nullable, uint8[rows]): a row with store_unless[row] == 0 is STORED (not added
+ * to) — the row-lazy step leaves rows outside its touched set unwritten. */
 int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
                            int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
-                           const float* C2, float* c2buf, uint8_t* c2flag, int32_t* overflow, lgcn_stream_t stream);
+                           const float* C2, float* c2buf, uint8_t* c2flag, int32_t* overflow,
+                           const uint8_t* store_unless, lgcn_stream_t stream);
 int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, const float* c2buf,
                           const uint8_t* c2flag, int32_t d, float* out_lo, float* out_hi, int64_t split,
                           lgcn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Row-lazy Adam (lgcn_rowadam.hip) for the sparse batch step: exact replay of the zero-gradient
+ * steps a row missed, when the row is next touched (reference utils/train_test.py:95-96; same
+ * element arithmetic as lgcn_adam_step). Tables p/g/m/v are (lo, hi) split at `split` rows of d.
+ *   lgcn_adam_consts: consts[t] = (float(-lr / (1 - beta1^t)), float(sqrt(1 - beta2^t))),
+ *     t in [t0, t1] (float pairs), the lgcn_adam_prologue formulas.
+ *   lgcn_row_adam: rows = rows_a[0..n_a) then keys_b[j] + off_b (j counted only if first_b[j]
+ *     and !skip_b[row], when those are given). *step = completed steps (device int64).
+ *     mode 0: catch the rows up to *step (duplicates handled by claim stamps, claim initialised
+ *     to -1); mode 1: catch up, then apply step *step + 1 with the gradient times clip[1]
+ *     (clip nullable), then ++*step (rows must be unique); mode 2: every row of [0, n_rows) up
+ *     to *step. last[r] = the last step applied to row r.
+ *   lgcn_row_grad_norm: out = (||g over the listed rows||, min(max_norm / (norm + 1e-6), 1)). */
+int lgcn_adam_consts(float* consts, int64_t t0, int64_t t1, float lr, double beta1, double beta2,
+                     lgcn_stream_t stream);
+int lgcn_row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_lo, float* m_hi, float* v_lo,
+                  float* v_hi, int64_t split, int32_t d, const int32_t* rows_a, int64_t n_a, const int64_t* keys_b,
+                  int64_t n_b, int64_t off_b, const uint8_t* first_b, const uint8_t* skip_b, int64_t n_rows,
+                  int32_t* last, int32_t* claim, int64_t* step, const float* consts, float one_minus_beta1,
+                  float beta2, float one_minus_beta2, float eps, const float* clip, int32_t mode,
+                  lgcn_stream_t stream);
+int lgcn_row_grad_norm_workspace_floats(void);
+int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
+                       int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
+                       const uint8_t* skip_b, float max_norm, float* ws, float* out, lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Recall@k (reference utils/train_test.py:165-212, compute_recall_at_k, called from evaluate

@@ -237,7 +237,8 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                                                             int32_t d, float* out_lo, float* out_hi, int64_t split,
                                                             float mul, float div, const float* __restrict__ C2,
                                                             float* __restrict__ c2buf, uint8_t* __restrict__ c2flag,
-                                                            int* __restrict__ overflow) {
+                                                            int* __restrict__ overflow,
+                                                            const uint8_t* __restrict__ store_unless) {
     constexpr int GPB = kRSBlock / LPR;
     __shared__ int lkey[kRangeCap];
     __shared__ int lidx[kRangeCap];
@@ -342,11 +343,18 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
             }
             const int64_t row = lo + key + key_offset;
             float4* o = reinterpret_cast<float4*>(srow(out_lo, out_hi, split, row, int64_t(d))) + l;
+            if (store_unless && !store_unless[row]) {  // row not written before: store
 #pragma unroll
-            for (int k = 0; k < NV; ++k) {
-                const float4 v = o[k * LPR];
-                o[k * LPR] = make_float4(v.x + (acc[k].x * mul) / div, v.y + (acc[k].y * mul) / div,
-                                         v.z + (acc[k].z * mul) / div, v.w + (acc[k].w * mul) / div);
+                for (int k = 0; k < NV; ++k)
+                    o[k * LPR] = make_float4((acc[k].x * mul) / div, (acc[k].y * mul) / div, (acc[k].z * mul) / div,
+                                             (acc[k].w * mul) / div);
+            } else {
+#pragma unroll
+                for (int k = 0; k < NV; ++k) {
+                    const float4 v = o[k * LPR];
+                    o[k * LPR] = make_float4(v.x + (acc[k].x * mul) / div, v.y + (acc[k].y * mul) / div,
+                                             v.z + (acc[k].z * mul) / div, v.w + (acc[k].w * mul) / div);
+                }
             }
         }
         __syncthreads();
@@ -380,7 +388,7 @@ __global__ __launch_bounds__(kBlock) void k_flagged_rows_add(const int64_t* __re
 template <int LPR, int NV>
 int launch_rs(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C, int32_t d, float* lo,
               float* hi, int64_t split, float mul, float div, const float* C2, float* c2buf, uint8_t* c2flag,
-              int* overflow, hipStream_t s) {
+              int* overflow, const uint8_t* store_unless, hipStream_t s) {
     // every workgroup streams all B keys once; enough workgroups that each keeps ~<= 256 entries
     // on average (the list holds kRangeCap), at least 256 (one per CU)
     int64_t wgs = B / 256 + 1;
@@ -394,7 +402,7 @@ int launch_rs(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset,
     }
     k_range_scatter<LPR, NV><<<dim3(static_cast<unsigned>(grid)), kRSBlock, 0, s>>>(keys, B, nrows, span, key_offset, C, d,
                                                                                  lo, hi, split, mul, div, C2, c2buf,
-                                                                                 c2flag, overflow);
+                                                                                 c2flag, overflow, store_unless);
     return check_launch("k_range_scatter");
 }
 
@@ -459,14 +467,15 @@ int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split, const 
 
 int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
                            int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
-                           const float* C2, float* c2buf, uint8_t* c2flag, int32_t* overflow, lgcn_stream_t stream) {
+                           const float* C2, float* c2buf, uint8_t* c2flag, int32_t* overflow,
+                           const uint8_t* store_unless, lgcn_stream_t stream) {
     if (B < 0 || d <= 0 || nrows < 0 || (B > 0 && (!keys || !C || !out_lo)) || (C2 && (!c2buf || !c2flag)))
         return fail(LGCN_E_ARG, "lgcn_range_scatter_add: bad args");
     if (B == 0 || nrows == 0) return LGCN_OK;
     if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C2 && (!al16(C2) || !al16(c2buf))))
         return fail(LGCN_E_UNSUPPORTED, "lgcn_range_scatter_add: needs d %% 4 == 0 and aligned rows");
     hipStream_t s = as_stream(stream);
-#define LGCN_RS(L, V) launch_rs<L, V>(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, c2buf, c2flag, overflow, s)
+#define LGCN_RS(L, V) launch_rs<L, V>(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, c2buf, c2flag, overflow, store_unless, s)
     switch (d) {
         case 16: return LGCN_RS(4, 1);
         case 32: return LGCN_RS(8, 1);

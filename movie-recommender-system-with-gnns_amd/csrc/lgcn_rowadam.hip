@@ -1,0 +1,323 @@
+// Row-lazy Adam for the two embedding tables of the sparse Cluster-GCN batch step
+// (reference utils/train_test.py:95-96: clip_grad_norm_(1) + optim.Adam(lr=1e-3), dense on
+// [U, d] + [I, d] every step).
+//
+// A row with a zero gradient still moves under Adam (m and v decay, p steps by m/denom), but its
+// update is a fixed function of (p, m, v, step constants): applied later, in order, it gives the
+// same floats. So a row is brought up to date only when it is next touched — replaying its missed
+// zero-gradient steps with exactly the arithmetic the dense kernel (lgcn_optim.hip adam_elem) uses
+// — and the rows a batch never reaches are not streamed every step. lgcn_row_adam_flush replays
+// every row up to the current step (epoch end / before parameters are read).
+//
+//   last[r]   the last step applied to row r (int32 per global row id)
+//   consts[t] (step_size_t, bc2_sqrt_t), t = 1..T: the per-step constants, filled by
+//             lgcn_adam_consts with the same double formulas as lgcn_adam_prologue
+//   step      device int64: the number of completed steps (capturable; lgcn_row_adam_update
+//             advances it)
+//
+// Rows live in two tables (r < split: lo[r], else hi[r - split]) like everywhere else.
+
+#include "lgcn_common.h"
+
+using namespace lgcn;
+
+namespace {
+
+struct RowTables {
+    float* p_lo;
+    float* p_hi;
+    float* g_lo;
+    float* g_hi;
+    float* m_lo;
+    float* m_hi;
+    float* v_lo;
+    float* v_hi;
+    int64_t split;
+    int32_t d;
+};
+
+struct RowList {
+    const int32_t* rows_a;   // row ids
+    int64_t n_a;
+    const int64_t* keys_b;   // rows keys_b[j] + off_b
+    int64_t n_b;
+    int64_t off_b;
+    const uint8_t* first_b;  // nullable: entry j counts only if first_b[j] (its key's first occurrence)
+    const uint8_t* skip_b;   // nullable: ... and !skip_b[row] (the row is already in list a)
+};
+
+struct AdamK {
+    float omb1, beta2, omb2, eps;
+};
+
+template <class T>
+__device__ __forceinline__ T* trow(T* lo, T* hi, int64_t split, int64_t r, int64_t d) {
+    return r < split ? lo + r * d : hi + (r - split) * d;
+}
+
+// the dense kernel's element update (lgcn_optim.hip adam_elem), verbatim
+__device__ __forceinline__ void adam_elem(float& p, float& g, float& m, float& v, float coef, float step_size,
+                                          float bc2_sqrt, const AdamK& k) {
+    g = g * coef;
+    m = m + k.omb1 * (g - m);
+    v = v * k.beta2;
+    v = v + k.omb2 * (g * g);
+    const float denom = sqrtf(v) / bc2_sqrt + k.eps;
+    p = p + step_size * (m / denom);
+}
+
+__device__ __forceinline__ bool list_row(const RowList& L, int64_t i, int64_t& row) {
+    if (i < L.n_a) {
+        row = L.rows_a[i];
+        return true;
+    }
+    const int64_t j = i - L.n_a;
+    row = L.keys_b[j] + L.off_b;
+    if (L.first_b && !L.first_b[j]) return false;
+    if (L.skip_b && L.skip_b[row]) return false;
+    return true;
+}
+
+__global__ void k_adam_consts(float2* __restrict__ consts, int64_t t0, int64_t t1, float lr, double beta1,
+                              double beta2) {
+    const int64_t t = t0 + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t > t1) return;
+    const double bc1 = 1.0 - pow(beta1, double(t));
+    const double bc2 = 1.0 - pow(beta2, double(t));
+    consts[t] = make_float2(static_cast<float>(-(static_cast<double>(lr) / bc1)), static_cast<float>(sqrt(bc2)));
+}
+
+// One LPR-lane group per list entry (or per row for the flush). mode 0: catch the row up to
+// step[0] with zero-gradient replays (duplicates skipped through claim stamps). mode 1: catch up
+// to step[0] then apply step[0]+1 with the row's gradient (the list must be duplicate-free:
+// first_b / skip_b). mode 2 (flush): every row in [0, n_rows) up to step[0].
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int64_t n_rows, int32_t* __restrict__ last,
+                                                     int32_t* __restrict__ claim, const int64_t* __restrict__ step,
+                                                     const float2* __restrict__ consts, AdamK k,
+                                                     const float* __restrict__ clip, int mode) {
+    constexpr int GPB = kBlock / LPR;
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    const int64_t i = int64_t(blockIdx.x) * GPB + g;
+    const int64_t t = step[0];
+    int64_t row;
+    if (mode == 2) {
+        if (i >= n_rows) return;
+        row = i;
+    } else {
+        if (i >= L.n_a + L.n_b) return;
+        if (!list_row(L, i, row)) return;
+        if (mode == 0) {
+            // duplicates in the catch-up list: the first claimer of this step's stamp does the work
+            int won = 0;
+            if (l == 0) won = atomicExch(claim + row, static_cast<int32_t>(2 * t)) != static_cast<int32_t>(2 * t);
+            won = __shfl(won, 0, LPR);
+            if (!won) return;
+        }
+    }
+    const int64_t from = int64_t(last[row]) + 1;
+    const int64_t upto = t;  // zero-gradient replays through step t
+    const float coef = (mode == 1 && clip) ? clip[1] : 1.0f;
+    const int64_t d = T.d;
+    float4* P = reinterpret_cast<float4*>(trow(T.p_lo, T.p_hi, T.split, row, d)) + l;
+    float4* M = reinterpret_cast<float4*>(trow(T.m_lo, T.m_hi, T.split, row, d)) + l;
+    float4* V = reinterpret_cast<float4*>(trow(T.v_lo, T.v_hi, T.split, row, d)) + l;
+    float4 p[NV], m[NV], v[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+        p[q] = P[q * LPR];
+        m[q] = M[q * LPR];
+        v[q] = V[q * LPR];
+    }
+    for (int64_t s = from; s <= upto; ++s) {
+        const float2 c = consts[s];
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            float z0 = 0.f, z1 = 0.f, z2 = 0.f, z3 = 0.f;
+            adam_elem(p[q].x, z0, m[q].x, v[q].x, 1.0f, c.x, c.y, k);
+            adam_elem(p[q].y, z1, m[q].y, v[q].y, 1.0f, c.x, c.y, k);
+            adam_elem(p[q].z, z2, m[q].z, v[q].z, 1.0f, c.x, c.y, k);
+            adam_elem(p[q].w, z3, m[q].w, v[q].w, 1.0f, c.x, c.y, k);
+        }
+    }
+    int32_t now = static_cast<int32_t>(upto);
+    if (mode == 1) {
+        const float2 c = consts[t + 1];
+        const float4* G = reinterpret_cast<const float4*>(trow(T.g_lo, T.g_hi, T.split, row, d)) + l;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            float4 gv = G[q * LPR];
+            adam_elem(p[q].x, gv.x, m[q].x, v[q].x, coef, c.x, c.y, k);
+            adam_elem(p[q].y, gv.y, m[q].y, v[q].y, coef, c.x, c.y, k);
+            adam_elem(p[q].z, gv.z, m[q].z, v[q].z, coef, c.x, c.y, k);
+            adam_elem(p[q].w, gv.w, m[q].w, v[q].w, coef, c.x, c.y, k);
+        }
+        now = static_cast<int32_t>(t + 1);
+    }
+    if (from <= upto || mode == 1) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            P[q * LPR] = p[q];
+            M[q * LPR] = m[q];
+            V[q * LPR] = v[q];
+        }
+    }
+    if (l == 0) last[row] = now;
+}
+
+// Sum of squares of the listed (duplicate-free) gradient rows: per-block partials, in a fixed
+// assignment (deterministic), finished by the dense path's k_norm_finish.
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_row_sqnorm(RowTables T, RowList L, float* __restrict__ partial) {
+    constexpr int GPB = kBlock / LPR;
+    __shared__ float red[kBlock / 64];
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    const int64_t n = L.n_a + L.n_b;
+    float acc = 0.f;
+    for (int64_t i = int64_t(blockIdx.x) * GPB + g; i < n; i += int64_t(gridDim.x) * GPB) {
+        int64_t row;
+        if (!list_row(L, i, row)) continue;
+        const float4* G = reinterpret_cast<const float4*>(trow(T.g_lo, T.g_hi, T.split, row, int64_t(T.d))) + l;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const float4 x = G[q * LPR];
+            acc += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float s = 0.f;
+        for (int w = 0; w < kBlock / 64; ++w) s += red[w];
+        partial[blockIdx.x] = s;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_norm_finish_rows(const float* __restrict__ partial, int nparts,
+                                                             float max_norm, float* __restrict__ out) {
+    __shared__ float red[kBlock / 64];
+    float acc = 0.f;
+    for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += partial[i];
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float s = 0.f;
+        for (int w = 0; w < kBlock / 64; ++w) s += red[w];
+        const float norm = sqrtf(s);
+        const float coef = max_norm / (norm + 1e-6f);
+        out[0] = norm;
+        out[1] = coef < 1.0f ? coef : 1.0f;
+    }
+}
+
+__global__ void k_step_advance(int64_t* step) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) step[0] += 1;
+}
+
+constexpr int kRowNormBlocks = 512;
+
+template <int LPR, int NV>
+int launch_row_adam(const RowTables& T, const RowList& L, int64_t n_rows, int32_t* last, int32_t* claim,
+                    const int64_t* step, const float2* consts, const AdamK& k, const float* clip, int mode,
+                    hipStream_t s) {
+    constexpr int GPB = kBlock / LPR;
+    const int64_t n = mode == 2 ? n_rows : L.n_a + L.n_b;
+    if (n <= 0) return LGCN_OK;
+    k_row_adam<LPR, NV><<<dim3(static_cast<unsigned>((n + GPB - 1) / GPB)), kBlock, 0, s>>>(T, L, n_rows, last, claim,
+                                                                                          step, consts, k, clip, mode);
+    return check_launch("k_row_adam");
+}
+
+template <int LPR, int NV>
+int launch_row_norm(const RowTables& T, const RowList& L, float max_norm, float* ws, float* out, hipStream_t s) {
+    k_row_sqnorm<LPR, NV><<<kRowNormBlocks, kBlock, 0, s>>>(T, L, ws);
+    if (int rc = check_launch("k_row_sqnorm")) return rc;
+    k_norm_finish_rows<<<1, kBlock, 0, s>>>(ws, kRowNormBlocks, max_norm, out);
+    return check_launch("k_norm_finish_rows");
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int check_tables(const RowTables& T, bool need_grad) {
+    if (!T.p_lo || !T.m_lo || !T.v_lo || T.d <= 0 || T.split < 0) return fail(LGCN_E_ARG, "lgcn_row_adam: bad tables");
+    if (need_grad && !T.g_lo) return fail(LGCN_E_ARG, "lgcn_row_adam: null gradient table");
+    const void* ps[] = {T.p_lo, T.p_hi, T.g_lo, T.g_hi, T.m_lo, T.m_hi, T.v_lo, T.v_hi};
+    for (const void* p : ps)
+        if (p && !al16(p)) return fail(LGCN_E_UNSUPPORTED, "lgcn_row_adam: tables must be 16-byte aligned");
+    return LGCN_OK;
+}
+
+#define LGCN_ROW_DISPATCH(CALL)                                                     \
+    switch (T.d) {                                                                  \
+        case 16: return CALL(4, 1);                                                 \
+        case 32: return CALL(8, 1);                                                 \
+        case 64: return CALL(16, 1);                                                \
+        case 128: return CALL(32, 1);                                               \
+        case 256: return CALL(64, 1);                                               \
+        case 512: return CALL(64, 2);                                               \
+        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_row_adam: d=%d", T.d);     \
+    }
+
+}  // namespace
+
+extern "C" {
+
+int lgcn_adam_consts(float* consts, int64_t t0, int64_t t1, float lr, double beta1, double beta2,
+                     lgcn_stream_t stream) {
+    if (!consts || t0 < 1 || t1 < t0) return fail(LGCN_E_ARG, "lgcn_adam_consts: bad range");
+    const int64_t n = t1 - t0 + 1;
+    k_adam_consts<<<grid_for(n, kBlock, int64_t(1) << 30), kBlock, 0, as_stream(stream)>>>(
+        reinterpret_cast<float2*>(consts), t0, t1, lr, beta1, beta2);
+    return check_launch("k_adam_consts");
+}
+
+int lgcn_row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_lo, float* m_hi, float* v_lo,
+                  float* v_hi, int64_t split, int32_t d, const int32_t* rows_a, int64_t n_a, const int64_t* keys_b,
+                  int64_t n_b, int64_t off_b, const uint8_t* first_b, const uint8_t* skip_b, int64_t n_rows,
+                  int32_t* last, int32_t* claim, int64_t* step, const float* consts, float one_minus_beta1,
+                  float beta2, float one_minus_beta2, float eps, const float* clip, int32_t mode,
+                  lgcn_stream_t stream) {
+    RowTables T{p_lo, p_hi, g_lo, g_hi, m_lo, m_hi, v_lo, v_hi, split, d};
+    if (int rc = check_tables(T, mode == 1)) return rc;
+    if (mode < 0 || mode > 2 || !last || !step || !consts || (mode == 0 && !claim) || n_a < 0 || n_b < 0 ||
+        (n_a > 0 && !rows_a) || (n_b > 0 && !keys_b))
+        return fail(LGCN_E_ARG, "lgcn_row_adam: bad args");
+    RowList L{rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b};
+    const AdamK k{one_minus_beta1, beta2, one_minus_beta2, eps};
+    hipStream_t s = as_stream(stream);
+    const auto* c2 = reinterpret_cast<const float2*>(consts);
+    int rc = LGCN_OK;
+#define LGCN_RA(LP, NVV) launch_row_adam<LP, NVV>(T, L, n_rows, last, claim, step, c2, k, clip, mode, s)
+    auto run = [&]() -> int { LGCN_ROW_DISPATCH(LGCN_RA) };
+#undef LGCN_RA
+    rc = run();
+    if (rc) return rc;
+    if (mode == 1) {  // the step is done: advance the device counter
+        k_step_advance<<<1, 64, 0, s>>>(step);
+        return check_launch("k_step_advance");
+    }
+    return LGCN_OK;
+}
+
+int lgcn_row_grad_norm_workspace_floats(void) { return kRowNormBlocks; }
+
+int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
+                       int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
+                       const uint8_t* skip_b, float max_norm, float* ws, float* out, lgcn_stream_t stream) {
+    RowTables T{nullptr, nullptr, const_cast<float*>(g_lo), const_cast<float*>(g_hi), nullptr, nullptr, nullptr,
+                nullptr, split, d};
+    if (!g_lo || !ws || !out || n_a < 0 || n_b < 0 || (n_a > 0 && !rows_a) || (n_b > 0 && !keys_b))
+        return fail(LGCN_E_ARG, "lgcn_row_grad_norm: bad args");
+    if (!al16(g_lo) || (g_hi && !al16(g_hi))) return fail(LGCN_E_UNSUPPORTED, "lgcn_row_grad_norm: alignment");
+    RowList L{rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b};
+    hipStream_t s = as_stream(stream);
+#define LGCN_RN(LP, NVV) launch_row_norm<LP, NVV>(T, L, max_norm, ws, out, s)
+    LGCN_ROW_DISPATCH(LGCN_RN)
+#undef LGCN_RN
+}
+
+}  // extern "C"

@@ -60,8 +60,14 @@ _SIGS = {
                        ctypes.c_int),
     "lgcn_bpr_loss": ([_vp, _i64, _i32, _f32, _vp, _vp], ctypes.c_int),
     "lgcn_segment_rows": ([_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _i32, _f32, _f32, _vp], ctypes.c_int),
-    "lgcn_range_scatter_add": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp],
-                               ctypes.c_int),
+    "lgcn_range_scatter_add": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp,
+                                _vp], ctypes.c_int),
+    "lgcn_adam_consts": ([_vp, _i64, _i64, _f32, ctypes.c_double, ctypes.c_double, _vp], ctypes.c_int),
+    "lgcn_row_adam": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64,
+                       _vp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _i32, _vp], ctypes.c_int),
+    "lgcn_row_grad_norm_workspace_floats": ([], ctypes.c_int),
+    "lgcn_row_grad_norm": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp],
+                           ctypes.c_int),
     "lgcn_recall_width": ([_i32, _vp, _vp], ctypes.c_int),
     "lgcn_normalize_rows": ([_vp, _vp, _i64, _i64, _i32, _vp, _i32, _i64, _vp], ctypes.c_int),
     "lgcn_score_filter": ([_vp, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp], ctypes.c_int),

@@ -96,3 +96,95 @@ class FusedAdam(torch.optim.Optimizer):
         _ffi.check(lib.lgcn_adam_step(arr, len(ps), 1 - beta1, beta2, 1 - beta2, group["eps"], step_size,
                                       bc2_sqrt, ctypes.c_void_p(clip_ptr) if clip_ptr else None, dev_scalars,
                                       1 if self.keep_clipped_grad else 0, stream), "lgcn_adam_step")
+
+
+class RowLazyAdam:
+    """Adam (+ clip_grad_norm_(max_norm)) over the two embedding tables, row-lazy and exact:
+    a row's missed zero-gradient steps are replayed (lgcn_row_adam) when the row is next touched,
+    with the arithmetic and per-step constants of FusedAdam(capturable=True), so after flush()
+    every row holds what FusedAdam would have produced; only the clip coefficient's last bits
+    can differ (its norm sums the touched rows only — the other rows' gradient is 0 — in another
+    order). Driven by lgcn_amd.train_step.FusedTrainStep(lazy=True) on one GPU; parameters are
+    stale between steps until flush() (call it before reading them: evaluation, checkpoints)."""
+
+    def __init__(self, user_w: torch.Tensor, item_w: torch.Tensor, lr: float = 1e-3, betas=(0.9, 0.999),
+                 eps: float = 1e-8, max_grad_norm: float | None = 1.0, max_steps: int = 1 << 24):
+        for t in (user_w, item_w):
+            _ffi.require_device(t, "RowLazyAdam")
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise TypeError("RowLazyAdam handles contiguous fp32 tables")
+        self.uw, self.iw = user_w, item_w
+        self.U, self.d = user_w.shape
+        self.N = self.U + item_w.shape[0]
+        self.lr, self.betas, self.eps, self.max_grad_norm = float(lr), betas, float(eps), max_grad_norm
+        dev = user_w.device
+        self.device = dev
+        self.m = (torch.zeros_like(user_w), torch.zeros_like(item_w))
+        self.v = (torch.zeros_like(user_w), torch.zeros_like(item_w))
+        self.last = torch.zeros(self.N, dtype=torch.int32, device=dev)
+        self.claim = torch.full((self.N,), -1, dtype=torch.int32, device=dev)
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.steps = 0  # host mirror of the completed steps
+        self.max_steps = int(max_steps)
+        self.consts = torch.empty((self.max_steps + 2, 2), dtype=torch.float32, device=dev)
+        lib = _ffi.load()
+        s = _ffi.stream_of(dev)
+        _ffi.check(lib.lgcn_adam_consts(self.consts.data_ptr(), 1, self.max_steps + 1, self.lr, float(betas[0]),
+                                        float(betas[1]), s), "lgcn_adam_consts")
+        self.norm_ws = torch.empty(lib.lgcn_row_grad_norm_workspace_floats(), dtype=torch.float32, device=dev)
+        self.last_norm = torch.zeros(2, dtype=torch.float32, device=dev)
+        # gradient tables: rows outside a step's touched set are never written or read
+        self.gu = torch.empty_like(user_w)
+        self.gi = torch.empty_like(item_w)
+
+    def _tables(self, with_grad: bool):
+        p = (self.uw.data_ptr(), self.iw.data_ptr())
+        g = (self.gu.data_ptr(), self.gi.data_ptr()) if with_grad else (None, None)
+        return (*p, *g, self.m[0].data_ptr(), self.m[1].data_ptr(), self.v[0].data_ptr(), self.v[1].data_ptr(),
+                self.U, self.d)
+
+    def _row_adam(self, rows_a, keys_b, off_b, first_b, skip_b, n_rows, clip, mode):
+        lib = _ffi.load()
+        b1, b2 = self.betas
+        na = rows_a.numel() if rows_a is not None else 0
+        nb = keys_b.numel() if keys_b is not None else 0
+        _ffi.check(lib.lgcn_row_adam(*self._tables(mode == 1), _ffi.ptr(rows_a), na, _ffi.ptr(keys_b), nb, off_b,
+                                     _ffi.ptr(first_b), _ffi.ptr(skip_b), n_rows, self.last.data_ptr(),
+                                     self.claim.data_ptr(), self.step_dev.data_ptr(), self.consts.data_ptr(),
+                                     1 - b1, b2, 1 - b2, self.eps, _ffi.ptr(clip), mode,
+                                     _ffi.stream_of(self.device)), "lgcn_row_adam")
+
+    def catch_up(self, rows_a: torch.Tensor, keys_b: torch.Tensor | None = None, off_b: int = 0) -> None:
+        """Bring the listed rows (duplicates allowed) up to the completed step count."""
+        self._row_adam(rows_a, keys_b, off_b, None, None, 0, None, 0)
+
+    def step_rows(self, rows_a: torch.Tensor, keys_b: torch.Tensor | None = None, off_b: int = 0,
+                  first_b: torch.Tensor | None = None, skip_b: torch.Tensor | None = None) -> None:
+        """One Adam step whose gradient (self.gu / self.gi) is zero outside the listed rows, which
+        must be duplicate-free (first_b / skip_b filter list b): clip norm over them, then the
+        update; rows not listed are deferred."""
+        if self.steps + 1 > self.max_steps:
+            raise RuntimeError(f"RowLazyAdam: more than max_steps={self.max_steps} steps")
+        lib = _ffi.load()
+        clip = None
+        if self.max_grad_norm is not None:
+            na = rows_a.numel()
+            nb = keys_b.numel() if keys_b is not None else 0
+            _ffi.check(lib.lgcn_row_grad_norm(self.gu.data_ptr(), self.gi.data_ptr(), self.U, self.d,
+                                              rows_a.data_ptr(), na, _ffi.ptr(keys_b), nb, off_b, _ffi.ptr(first_b),
+                                              _ffi.ptr(skip_b), float(self.max_grad_norm), self.norm_ws.data_ptr(),
+                                              self.last_norm.data_ptr(), _ffi.stream_of(self.device)),
+                       "lgcn_row_grad_norm")
+            clip = self.last_norm
+        self._row_adam(rows_a, keys_b, off_b, first_b, skip_b, 0, clip, 1)
+        self.steps += 1
+
+    def flush(self) -> None:
+        """Replay every row up to the completed step count (parameters are current after it)."""
+        self._row_adam(None, None, 0, None, None, self.N, None, 2)
+
+    def exp_avg(self) -> tuple[torch.Tensor, torch.Tensor]:
+        return self.m
+
+    def exp_avg_sq(self) -> tuple[torch.Tensor, torch.Tensor]:
+        return self.v

@@ -79,11 +79,12 @@ def _schedule(rowptr: torch.Tensor, N: int, E: int, chunk: int, side_split: int,
     return items, splits, n_items, n_splits, n_partials
 
 
-def segment_directions(keys: torch.Tensor, N: int, chunk: int = DEFAULT_CHUNK):
+def segment_directions(keys: torch.Tensor, N: int, chunk: int = DEFAULT_CHUNK, row_mask: torch.Tensor | None = None):
     """Plans for summing rows C[j] into output row keys[j] (j = 0..M-1) with lgcn_spmm, weight 1,
     in j order within a row: (dense: every row scheduled, for a SCALE/STORE pass that also writes
-    the empty rows; sparse: only rows with a contribution, for an ADD pass). Built once per
-    Cluster-GCN batch for its fixed (user, positive) gradient rows."""
+    the empty rows; sparse: only rows with a contribution, for an ADD pass; with row_mask also
+    masked: every masked row). Built once per Cluster-GCN batch for its fixed (user, positive)
+    gradient rows."""
     lib = _ffi.load()
     dev = keys.device
     M = keys.numel()
@@ -108,7 +109,11 @@ def segment_directions(keys: torch.Tensor, N: int, chunk: int = DEFAULT_CHUNK):
     sparse = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, mask, stream), chunk)
     if int(err.item()):
         raise IndexError("segment keys out of range")
-    return dense, sparse
+    if row_mask is None:
+        return dense, sparse
+    # every row of row_mask (0 where it has no contribution), e.g. a batch's touched rows
+    masked = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, row_mask, stream), chunk)
+    return dense, sparse, masked
 
 
 def _build_direction(key: torch.Tensor, other: torch.Tensor, N: int, chunk: int, side_split: int,

@@ -34,7 +34,7 @@ from .propagate import propagate_backward_seeded, propagate_forward, spmm
 
 
 class _BatchState:
-    def __init__(self, model, edge_index: torch.Tensor, d: int):
+    def __init__(self, model, edge_index: torch.Tensor, d: int, lazy: bool = False):
         dev = edge_index.device
         U, I = model.num_users, model.num_items
         N = U + I
@@ -56,8 +56,15 @@ class _BatchState:
         from .plan import segment_directions
 
         self.small = 2 * B <= N  # segment plans index contributions as node ids (always true for real batches)
-        if self.small:
+        self.lazy = lazy and self.small
+        if self.lazy:
+            # row-lazy optimizer: only the batch's touched rows (and the negatives) are written
+            self.fixed_dense, self.fixed_sparse, self.fixed_touched = segment_directions(
+                self.keys[:2 * B], N, chunk=32, row_mask=self.plan.touched)
+            self.touched_rows = torch.nonzero(self.plan.touched).squeeze(1).to(torch.int32).contiguous()
+        elif self.small:
             self.fixed_dense, self.fixed_sparse = segment_directions(self.keys[:2 * B], N, chunk=32)
+        if self.small:
             self.c2buf = torch.empty((B, d), dtype=torch.float32, device=dev)
             self.c2flag = torch.empty(B, dtype=torch.uint8, device=dev)
             self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -83,7 +90,7 @@ class FusedTrainStep:
     compute_grads(batch) -> loss: sets user/item_embedding.weight.grad only."""
 
     def __init__(self, model, optimizer, bpr_coeff: float = 5e-3, world: int = 1, max_entries: int = 4096,
-                 graphs: bool = False):
+                 graphs: bool = False, lazy: bool = False):
         """graphs=True: the first step of each batch runs eagerly, then the whole step (gradients
         and, at world == 1, the optimizer — which must be a capturable FusedAdam) is captured in a
         per-batch hipGraph and replayed from then on; negatives still come from the global CUDA
@@ -94,7 +101,13 @@ class FusedTrainStep:
         self.world = world
         self.max_entries = max_entries
         self.graphs = graphs
-        if graphs and world == 1 and not getattr(optimizer, "capturable", False):
+        self.lazy = lazy
+        if lazy:
+            from .optim import RowLazyAdam
+
+            if not isinstance(optimizer, RowLazyAdam) or world != 1:
+                raise ValueError("lazy=True needs a lgcn_amd.optim.RowLazyAdam and world == 1")
+        elif graphs and world == 1 and not getattr(optimizer, "capturable", False):
             raise ValueError("graphs=True needs a capturable optimizer (lgcn_amd.optim.FusedAdam(capturable=True))")
         self._states: dict[int, tuple[weakref.ref, int, _BatchState]] = {}
 
@@ -104,7 +117,7 @@ class FusedTrainStep:
             ref, ver, st = hit
             if ref() is edge_index and ver == edge_index._version:
                 return st
-        st = _BatchState(self.model, edge_index, self.model.dim_h)
+        st = _BatchState(self.model, edge_index, self.model.dim_h, lazy=self.lazy)
         self._states[id(edge_index)] = (weakref.ref(edge_index), edge_index._version, st)
         if len(self._states) > self.max_entries:
             for k in [k for k, (r, _, _) in self._states.items() if r() is None]:
@@ -148,7 +161,7 @@ class FusedTrainStep:
                 _ffi.check(lib.lgcn_range_scatter_add(st.neg.data_ptr(), B, I, U, st.cf[2 * B:].data_ptr(), d,
                                                       gu.data_ptr(), gi.data_ptr(), U, mul, div,
                                                       st.cw[2 * B:].data_ptr(), st.c2buf.data_ptr(),
-                                                      st.c2flag.data_ptr(), st.overflow.data_ptr(), stream),
+                                                      st.c2flag.data_ptr(), st.overflow.data_ptr(), None, stream),
                            "lgcn_range_scatter_add")
                 propagate_backward_seeded(gu, gi, st.plan, K)
                 spmm(st.fixed_sparse, N, d, (st.cw, None, big), None, grads, None, _ffi.EPI_ADD, stream=stream)
@@ -171,6 +184,60 @@ class FusedTrainStep:
         iw.grad = gi
         return st.loss
 
+    def _step_lazy(self, st: _BatchState) -> torch.Tensor:
+        """The whole batch step with the row-lazy optimizer: catch the batch's rows (touched rows
+        and this step's negatives) up, forward, loss, gradient rows written only where the step
+        can make them nonzero, backward, clip + Adam on exactly those rows."""
+        m = self.model
+        opt = self.optimizer
+        lib = _ffi.load()
+        uw, iw = m.user_embedding.weight, m.item_embedding.weight
+        U, I, K, d = m.num_users, m.num_items, m.num_layers, m.dim_h
+        N = U + I
+        B = st.B
+        dev = uw.device
+        stream = _ffi.stream_of(dev)
+        div = float(K + 1)
+        mul = float(np.float32(1.0 / (K + 1)))
+        big = 1 << 62
+        with torch.no_grad():
+            torch.randint(0, I, (B,), device=dev, out=st.neg)
+            torch.add(st.neg, U, out=st.keys[2 * B:])
+            opt.catch_up(st.touched_rows, st.neg, U)
+            out = propagate_forward(uw.detach(), iw.detach(), st.plan, K)
+            _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
+                                          st.users.data_ptr(), st.pos.data_ptr(), st.neg.data_ptr(), B, d,
+                                          st.plan.touched.data_ptr(), div, mul,
+                                          self.coeff, st.cf.data_ptr(), st.cw.data_ptr(), st.terms.data_ptr(),
+                                          stream), "lgcn_bpr_fused")
+            _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(), stream),
+                       "lgcn_bpr_loss")
+            gu, gi = opt.gu, opt.gi
+            grads = (gu, gi, U)
+            # seed g = (dF * mul) / div on every touched row (0 where no (user, positive) key)...
+            spmm(st.fixed_touched, N, d, (st.cf, None, big), None, grads, None, _ffi.EPI_SCALE, div, mul,
+                 stream=stream)
+            # ... the negatives' rows added (stored where the row is outside the touched set)
+            _ffi.check(lib.lgcn_range_scatter_add(st.neg.data_ptr(), B, I, U, st.cf[2 * B:].data_ptr(), d,
+                                                  gu.data_ptr(), gi.data_ptr(), U, mul, div,
+                                                  st.cw[2 * B:].data_ptr(), st.c2buf.data_ptr(),
+                                                  st.c2flag.data_ptr(), st.overflow.data_ptr(),
+                                                  st.plan.touched.data_ptr(), stream), "lgcn_range_scatter_add")
+            propagate_backward_seeded(gu, gi, st.plan, K)
+            spmm(st.fixed_sparse, N, d, (st.cw, None, big), None, grads, None, _ffi.EPI_ADD, stream=stream)
+            _ffi.check(lib.lgcn_flagged_rows_add(st.neg.data_ptr(), B, U, st.c2buf.data_ptr(),
+                                                 st.c2flag.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U,
+                                                 stream), "lgcn_flagged_rows_add")
+            # rows with a possibly nonzero gradient, each once: touched rows, then negatives at
+            # their first occurrence that are not touched
+            opt.step_rows(st.touched_rows, st.neg, U, first_b=st.c2flag, skip_b=st.plan.touched)
+        return st.loss
+
+    def sync(self) -> None:
+        """Make the parameters current (row-lazy optimizer: replay every deferred row)."""
+        if self.lazy:
+            self.optimizer.flush()
+
     def check_overflow(self) -> None:
         """Raise if any step's negative scatter overflowed a workgroup list (never expected for
         uniform negatives; one host read per batch state — call once per epoch)."""
@@ -189,6 +256,27 @@ class FusedTrainStep:
         allreduce_grads([self.model.user_embedding.weight, self.model.item_embedding.weight], self.world)
 
     def step(self, batch) -> torch.Tensor:
+        if self.lazy:
+            st = self.state(batch.edge_index)
+            if not st.lazy:
+                raise ValueError("lazy step needs a batch with 2B <= N")
+            if not self.graphs:
+                return self._step_lazy(st)
+            if getattr(st, "graph", None) is None:
+                loss = self._step_lazy(st)  # real first step (warms allocations), then capture
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                steps = self.optimizer.steps
+                with torch.cuda.graph(g):
+                    st.graph_loss = self._step_lazy(st)
+                self.optimizer.steps = steps  # the capture ran no step
+                st.graph = g
+                return loss
+            if self.optimizer.steps + 1 > self.optimizer.max_steps:
+                raise RuntimeError("RowLazyAdam: max_steps exceeded")
+            st.graph.replay()
+            self.optimizer.steps += 1
+            return st.graph_loss
         if not self.graphs:
             loss = self.compute_grads(batch)
             if self.world > 1:

@@ -45,7 +45,7 @@ def _run(gpu, keys_np, nrows, off, d, N, mul, div, with_c2=True, seed=0):
     _ffi.check(lib.lgcn_range_scatter_add(keys.data_ptr(), B, nrows, off, Cg.data_ptr(), d, lo.data_ptr(),
                                           hi.data_ptr(), split, mul, div,
                                           C2g.data_ptr() if with_c2 else None, buf.data_ptr(), flag.data_ptr(),
-                                          ovf.data_ptr(), s), "lgcn_range_scatter_add")
+                                          ovf.data_ptr(), None, s), "lgcn_range_scatter_add")
     after1 = torch.cat([lo, hi]).cpu().numpy()
     if with_c2:
         _ffi.check(lib.lgcn_flagged_rows_add(keys.data_ptr(), B, off, buf.data_ptr(), flag.data_ptr(), d,

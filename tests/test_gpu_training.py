@@ -216,3 +216,92 @@ def test_graph_replay_equals_eager(gpu):
         res.append((losses, m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+
+
+@pytest.mark.parametrize("clip", [None, 1.0])
+def test_row_lazy_adam_matches_dense_fused_adam(gpu, clip):
+    """RowLazyAdam (deferred rows replayed when touched, flush at the end) == dense
+    FusedAdam(capturable=True) on the same sparse gradients: bitwise without clipping (the
+    replays are the dense kernel's arithmetic with its per-step constants); with clipping the
+    norm is summed over other rows in another order, so to fp32 rounding of the clip coef."""
+    from lgcn_amd.optim import FusedAdam, RowLazyAdam
+
+    U, I, d = 300, 200, 64
+    N = U + I
+    torch.manual_seed(0)
+    w0 = [torch.randn(U, d, device=gpu) * 0.1, torch.randn(I, d, device=gpu) * 0.1]
+    dense = [torch.nn.Parameter(t.clone()) for t in w0]
+    lazy = [t.clone() for t in w0]
+    od = FusedAdam(dense, lr=1e-2, max_grad_norm=clip, capturable=True)
+    ol = RowLazyAdam(lazy[0], lazy[1], lr=1e-2, max_grad_norm=clip)
+    rng = np.random.default_rng(1)
+    for step in range(15):
+        rows = np.unique(rng.integers(0, N, rng.integers(1, 120)))
+        negs = rng.integers(0, I, 40)  # list b: item ids, duplicates and overlaps allowed
+        gfull = torch.zeros(N, d, device=gpu)
+        live = np.unique(np.concatenate([rows, negs + U]))
+        gfull[torch.from_numpy(live).to(gpu)] = torch.randn(len(live), d, device=gpu) * (3.0 if step % 3 else 0.05)
+        dense[0].grad, dense[1].grad = gfull[:U].clone(), gfull[U:].clone()
+        ra = torch.from_numpy(rows.astype(np.int32)).to(gpu)
+        nb = torch.from_numpy(negs).to(gpu)
+        ol.catch_up(ra, nb, U)
+        ol.gu.copy_(gfull[:U])
+        ol.gi.copy_(gfull[U:])
+        first = np.zeros(len(negs), np.uint8)
+        _, idx = np.unique(negs, return_index=True)
+        first[idx] = 1
+        skip = np.zeros(N, np.uint8)
+        skip[rows] = 1
+        ol.step_rows(ra, nb, U, first_b=torch.from_numpy(first).to(gpu), skip_b=torch.from_numpy(skip).to(gpu))
+        od.step()
+    ol.flush()
+    for a, b in zip(dense, lazy):
+        if clip is None:
+            assert torch.equal(a.detach(), b)
+        else:
+            assert (a.detach() - b).abs().max().item() <= 1e-6 * a.abs().max().item()
+
+
+@pytest.mark.parametrize("use_graphs,clip", [(False, float("inf")), (True, float("inf")), (False, 1.0)])
+def test_lazy_train_step_matches_dense_step(gpu, use_graphs, clip):
+    """FusedTrainStep(lazy=True) + RowLazyAdam == FusedTrainStep + dense capturable FusedAdam on
+    the same Cluster-GCN batches and negatives. Without clipping (max_norm = inf, coefficient
+    exactly 1): bitwise, every loss and every parameter (eager and hipGraph-replayed). With clip_grad_norm_(1): the two norms sum the same
+    squares in different orders, so the coefficient can differ in its last bit, and Adam's
+    sign-like update carries that into elements whose gradient is at noise level — losses to
+    1e-5 and parameters to 1e-3 of their scale after 20 steps."""
+    from lgcn_amd import cluster as C
+    from lgcn_amd.optim import FusedAdam, RowLazyAdam
+    from lgcn_amd.train_step import FusedTrainStep
+    from models.light_gcn import LightGCN
+
+    import graphs
+
+    U, I, ei = graphs.subsampled(U=2000, I=1000, pairs=8000, seed=4)
+    part = C.partition_nodes(ei, U + I, 8)
+    batches = [_Batch(torch.from_numpy(x).to(gpu)) for x in C.intra_part_edges(ei, part, 8)]
+    assert all(2 * int((b.edge_index[0] < U).sum()) <= U + I for b in batches)
+    res = []
+    for lazy in (False, True):
+        torch.manual_seed(0)
+        m = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
+        if lazy:
+            opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-2,
+                              max_grad_norm=clip)
+        else:
+            opt = FusedAdam(m.parameters(), lr=1e-2, max_grad_norm=clip, capturable=True)
+        step = FusedTrainStep(m, opt, graphs=use_graphs, lazy=lazy)
+        losses = []
+        for i in range(20):
+            torch.cuda.manual_seed(100 + i)
+            losses.append(step.step(batches[i % 8]).item())
+        step.sync()
+        res.append((losses, m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone()))
+    if clip == float("inf"):
+        assert res[0][0] == res[1][0]
+        assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+        return
+    for a, b in zip(res[0][0], res[1][0]):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(a))
+    for x, y in ((res[0][1], res[1][1]), (res[0][2], res[1][2])):
+        assert (x - y).abs().max().item() <= 1e-3 * x.abs().max().item()
