@@ -175,6 +175,21 @@ int lgcn_spmm_combine(const lgcn_item_t* items, int64_t n_items,
                       float* acc_lo, float* acc_hi, int64_t acc_split,
                       float* partial, int32_t mode, float div, float mul,
                       lgcn_stream_t stream);
+/* Source-sliced schedule (lgcn_amd/sliced.py): S slices of the source id range, bounds[0..S]
+ * (device int64, bounds[0] = 0, bounds[S] = N, S <= 250). Every row's CSR run is cut where its
+ * neighbour's slice changes; a row with a segment longer than chunk is a hub (its segments are
+ * chunked into partial slots, finished by lgcn_spmm_combine via splits), any other row gets one
+ * item per segment with FIRST/LAST flags (an empty row one flag-only item in slice 0). Items are
+ * sorted slice-major, longest first; offsets[s] (device int64[S+1]) is slice s's first item.
+ * counts = {n_items, n_splits, n_partials, unsorted}: unsorted != 0 if some row's neighbours are
+ * not ascending (the chain could not follow CSR order; use the plain schedule). */
+int lgcn_slice_schedule_workspace_size(int64_t E, int64_t N, int32_t S, int32_t chunk, size_t* bytes,
+                                       int64_t* items_cap);
+int lgcn_slice_schedule_build(const int64_t* rowptr, const int32_t* col, int64_t N, int64_t E,
+                              const int64_t* bounds, int32_t S, int32_t chunk, lgcn_item_t* items, int64_t items_cap,
+                              int64_t* offsets, lgcn_split_t* splits, int64_t splits_cap, int64_t* counts,
+                              void* ws, size_t ws_bytes, lgcn_stream_t stream);
+
 /* One launch of a source-sliced schedule (the item pass only). Row items carry flags in the high
  * bits of len: 0x20000000 = the row's FIRST segment (its sum starts at 0, else it continues from
  * run[row]), 0x40000000 = its LAST segment (the epilogue runs, else the running sum is stored to

@@ -158,6 +158,150 @@ __global__ void k_sched_gather(const lgcn_item_t* __restrict__ raw, const int32_
         items[m] = raw[idx[m]];
 }
 
+// ---- source-sliced schedule (lgcn_slice_schedule_build; see lgcn_amd/sliced.py) ----
+constexpr int32_t kSliceFirst = 0x20000000;
+constexpr int32_t kSliceLast = 0x40000000;
+
+__device__ __forceinline__ int slice_of(int64_t c, const int64_t* __restrict__ bounds, int S) {
+    // bounds[0] = 0 < bounds[1] < ... < bounds[S] = N: the s with bounds[s] <= c < bounds[s+1]
+    int lo = 0, hi = S - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (bounds[mid] <= c) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// One thread per row: its segments (runs of one source slice), hub flag (a segment longer than
+// chunk), item / partial counts, and whether its neighbours are ascending.
+__global__ void k_slice_count(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col, int64_t N,
+                              const int64_t* __restrict__ bounds, int S, int32_t chunk,
+                              int64_t* __restrict__ n_items, int32_t* __restrict__ n_part,
+                              int32_t* __restrict__ n_split, int32_t* __restrict__ unsorted) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += stride) {
+        const int64_t beg = rowptr[i], end = rowptr[i + 1];
+        if (end == beg) {
+            n_items[i] = 1;
+            n_part[i] = 0;
+            n_split[i] = 0;
+            continue;
+        }
+        int64_t segs = 0, chunks = 0, maxlen = 0, len = 0;
+        int cur = -1;
+        int32_t prev = -1;
+        bool bad = false;
+        for (int64_t e = beg; e < end; ++e) {
+            const int32_t c = col[e];
+            bad |= c < prev;
+            prev = c;
+            const int sl = slice_of(c, bounds, S);
+            if (sl != cur) {
+                if (len) {
+                    ++segs;
+                    chunks += (len + chunk - 1) / chunk;
+                    maxlen = len > maxlen ? len : maxlen;
+                }
+                cur = sl;
+                len = 0;
+            }
+            ++len;
+        }
+        ++segs;
+        chunks += (len + chunk - 1) / chunk;
+        maxlen = len > maxlen ? len : maxlen;
+        const bool hub = maxlen > chunk;
+        n_items[i] = hub ? chunks : segs;
+        n_part[i] = hub ? static_cast<int32_t>(chunks) : 0;
+        n_split[i] = hub ? 1 : 0;
+        if (bad) atomicOr(unsorted, 1);
+    }
+}
+
+__global__ void k_slice_fill(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col, int64_t N,
+                             const int64_t* __restrict__ bounds, int S, int32_t chunk,
+                             const int64_t* __restrict__ n_items, const int64_t* __restrict__ item_off,
+                             const int32_t* __restrict__ n_part, const int32_t* __restrict__ part_off,
+                             const int32_t* __restrict__ n_split, const int32_t* __restrict__ split_off,
+                             lgcn_item_t* __restrict__ raw, uint32_t* __restrict__ keys, int32_t* __restrict__ idx,
+                             lgcn_split_t* __restrict__ splits, int64_t* __restrict__ counts) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += stride) {
+        const int64_t beg = rowptr[i], end = rowptr[i + 1];
+        int64_t o = item_off[i];
+        auto emit = [&](int64_t b, int32_t lenflags, int32_t dst, int sl, int32_t len) {
+            lgcn_item_t it;
+            it.beg = b;
+            it.len = lenflags;
+            it.dst = dst;
+            raw[o] = it;
+            // slice-major, longest first inside a slice
+            const uint32_t l24 = static_cast<uint32_t>(len < 0xFFFFFF ? len : 0xFFFFFF);
+            keys[o] = (static_cast<uint32_t>(sl) << 24) | (0xFFFFFFu - l24);
+            idx[o] = static_cast<int32_t>(o);
+            ++o;
+        };
+        if (end == beg) {
+            emit(beg, kSliceFirst | kSliceLast, static_cast<int32_t>(i), 0, 0);
+        } else {
+            const bool hub = n_part[i] > 0;
+            int32_t pk = 0;  // hub rows: next partial slot, in CSR order
+            int64_t sb = beg;
+            int cur = slice_of(col[beg], bounds, S);
+            for (int64_t e = beg + 1; e <= end; ++e) {
+                const int sl = (e < end) ? slice_of(col[e], bounds, S) : -1;
+                if (sl == cur) continue;
+                const int64_t len = e - sb;  // segment [sb, e) in slice cur
+                if (hub) {
+                    for (int64_t c0 = 0; c0 < len; c0 += chunk) {
+                        const int32_t l = static_cast<int32_t>(len - c0 < chunk ? len - c0 : chunk);
+                        emit(sb + c0, l, -(part_off[i] + pk) - 1, cur, l);
+                        ++pk;
+                    }
+                } else {
+                    const int32_t flags = (sb == beg ? kSliceFirst : 0) | (e == end ? kSliceLast : 0);
+                    emit(sb, static_cast<int32_t>(len) | flags, static_cast<int32_t>(i), cur, static_cast<int32_t>(len));
+                }
+                sb = e;
+                cur = sl;
+            }
+            if (hub) {
+                lgcn_split_t sp;
+                sp.row = static_cast<int32_t>(i);
+                sp.pbeg = part_off[i];
+                sp.pcnt = n_part[i];
+                sp.pad = 0;
+                splits[split_off[i]] = sp;
+            }
+        }
+        if (i == N - 1) {
+            counts[0] = item_off[i] + n_items[i];
+            counts[1] = split_off[i] + n_split[i];
+            counts[2] = part_off[i] + n_part[i];
+        }
+    }
+}
+
+// offsets[s] = first sorted item of slice s (lower bound of s << 24), s = 0..S
+__global__ void k_slice_offsets(const uint32_t* __restrict__ skeys, int64_t n, int S, int64_t* __restrict__ offsets) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s > S) return;
+    const uint32_t key = static_cast<uint32_t>(s) << 24;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (skeys[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    offsets[s] = lo;  // offsets[S] = number of real items (padding keys sort after S << 24)
+}
+
+int64_t slice_items_cap(int64_t E, int64_t N, int S, int32_t chunk) {
+    const int64_t segs = E < N * int64_t(S) ? E : N * int64_t(S);
+    return segs + E / chunk + N + 1;
+}
+
 // sizes of the cub temp storage we need
 size_t csr_cub_bytes(int64_t E, int64_t N) {
     size_t t = 0;
@@ -333,6 +477,105 @@ int lgcn_schedule_build(const int64_t* rowptr, int64_t N, int64_t E, int32_t chu
     // gather all cap slots; the tail beyond n_items is padding the kernels never index
     k_sched_gather<<<grid_for(cap, kBlock, 8192), kBlock, 0, s>>>(raw, i_out, cap, items);
     return check_launch("k_sched_gather");
+}
+
+
+int lgcn_slice_schedule_workspace_size(int64_t E, int64_t N, int32_t S, int32_t chunk, size_t* bytes,
+                                       int64_t* items_cap) {
+    if (!bytes || E < 0 || N < 0 || S < 1 || S > 250 || chunk < 1)
+        return fail(LGCN_E_ARG, "lgcn_slice_schedule_workspace_size: bad args");
+    const int64_t cap = slice_items_cap(E, N, S, chunk);
+    if (items_cap) *items_cap = cap;
+    size_t a = 0, b = 0, c = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, (const int64_t*)nullptr, (int64_t*)nullptr,
+                                           static_cast<int>(N > 0 ? N : 1));
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                           static_cast<int>(N > 0 ? N : 1));
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, static_cast<int>(cap), 0,
+                                             32);
+    size_t m = a > b ? a : b;
+    m = m > c ? m : c;
+    Carver cv{nullptr, 0};
+    cv.take<int64_t>(N);
+    cv.take<int64_t>(N);
+    cv.take<int32_t>(N);
+    cv.take<int32_t>(N);
+    cv.take<int32_t>(N);
+    cv.take<int32_t>(N);
+    cv.take<lgcn_item_t>(cap);
+    cv.take<uint32_t>(cap);
+    cv.take<uint32_t>(cap);
+    cv.take<int32_t>(cap);
+    cv.take<int32_t>(cap);
+    cv.take<char>(m);
+    *bytes = cv.used + 256;
+    return LGCN_OK;
+}
+
+int lgcn_slice_schedule_build(const int64_t* rowptr, const int32_t* col, int64_t N, int64_t E,
+                              const int64_t* bounds, int32_t S, int32_t chunk, lgcn_item_t* items, int64_t items_cap,
+                              int64_t* offsets, lgcn_split_t* splits, int64_t splits_cap, int64_t* counts,
+                              void* ws, size_t ws_bytes, lgcn_stream_t stream) {
+    if (!rowptr || !bounds || !counts || !offsets || N <= 0 || E < 0 || S < 1 || S > 250 || chunk < 1 ||
+        chunk >= (1 << 24) || (E > 0 && !col))
+        return fail(LGCN_E_ARG, "lgcn_slice_schedule_build: bad args");
+    if (N > INT32_MAX || E > INT32_MAX) return fail(LGCN_E_UNSUPPORTED, "slice schedule: sizes exceed int32");
+    hipStream_t s = as_stream(stream);
+    const int64_t cap = slice_items_cap(E, N, S, chunk);
+    if (!items || items_cap < cap || !splits || splits_cap < N)
+        return fail(LGCN_E_ARG, "lgcn_slice_schedule_build: items_cap %lld < %lld or splits_cap %lld < %lld",
+                    (long long)items_cap, (long long)cap, (long long)splits_cap, (long long)N);
+    Carver c{static_cast<char*>(ws), ws_bytes};
+    int64_t* n_items = c.take<int64_t>(N);
+    int64_t* item_off = c.take<int64_t>(N);
+    int32_t* n_part = c.take<int32_t>(N);
+    int32_t* part_off = c.take<int32_t>(N);
+    int32_t* n_split = c.take<int32_t>(N);
+    int32_t* split_off = c.take<int32_t>(N);
+    lgcn_item_t* raw = c.take<lgcn_item_t>(cap);
+    uint32_t* k_in = c.take<uint32_t>(cap);
+    uint32_t* k_out = c.take<uint32_t>(cap);
+    int32_t* i_in = c.take<int32_t>(cap);
+    int32_t* i_out = c.take<int32_t>(cap);
+    size_t a = 0, b = 0, cb = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, (const int64_t*)nullptr, (int64_t*)nullptr, static_cast<int>(N));
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr, static_cast<int>(N));
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, static_cast<int>(cap), 0, 32);
+    size_t cub_bytes = a > b ? a : b;
+    cub_bytes = cub_bytes > cb ? cub_bytes : cb;
+    void* cub_tmp = c.take<char>(cub_bytes);
+    if (!c.ok) return fail(LGCN_E_WORKSPACE, "lgcn_slice_schedule_build: workspace %zu < %zu", ws_bytes, c.used);
+    // counts[3] = 1 if some row's neighbours are not ascending (the caller falls back)
+    if (int rc = check_hip(hipMemsetAsync(counts, 0, 4 * sizeof(int64_t), s), "memset counts")) return rc;
+    const unsigned g = grid_for(N, kBlock, 8192);
+    k_slice_count<<<g, kBlock, 0, s>>>(rowptr, col, N, bounds, S, chunk, n_items, n_part, n_split,
+                                       reinterpret_cast<int32_t*>(counts + 3));
+    if (int rc = check_launch("k_slice_count")) return rc;
+    size_t t = cub_bytes;
+    if (int rc = check_hip(hipcub::DeviceScan::ExclusiveSum(cub_tmp, t, n_items, item_off, static_cast<int>(N), s), "scan items")) return rc;
+    t = cub_bytes;
+    if (int rc = check_hip(hipcub::DeviceScan::ExclusiveSum(cub_tmp, t, n_part, part_off, static_cast<int>(N), s), "scan parts")) return rc;
+    t = cub_bytes;
+    if (int rc = check_hip(hipcub::DeviceScan::ExclusiveSum(cub_tmp, t, n_split, split_off, static_cast<int>(N), s), "scan splits")) return rc;
+    k_fill_u32<<<grid_for(cap, kBlock, 8192), kBlock, 0, s>>>(k_in, cap, 0xFFFFFFFFu);
+    if (int rc = check_launch("k_fill_u32")) return rc;
+    k_fill_u32<<<grid_for(cap, kBlock, 8192), kBlock, 0, s>>>(reinterpret_cast<uint32_t*>(i_in), cap, 0u);
+    if (int rc = check_launch("k_fill_u32")) return rc;
+    k_slice_fill<<<g, kBlock, 0, s>>>(rowptr, col, N, bounds, S, chunk, n_items, item_off, n_part, part_off, n_split,
+                                      split_off, raw, k_in, i_in, splits, counts);
+    if (int rc = check_launch("k_slice_fill")) return rc;
+    t = cub_bytes;
+    if (int rc = check_hip(hipcub::DeviceRadixSort::SortPairs(cub_tmp, t, k_in, k_out, i_in, i_out,
+                                                              static_cast<int>(cap), 0, 32, s),
+                           "SortPairs(slice schedule)"))
+        return rc;
+    k_sched_gather<<<grid_for(cap, kBlock, 8192), kBlock, 0, s>>>(raw, i_out, cap, items);
+    if (int rc = check_launch("k_sched_gather")) return rc;
+    // offsets over the sorted keys; padding keys (0xFFFFFFFF) sort after every real slice
+    k_slice_offsets<<<1, 256, 0, s>>>(k_out, cap, S, offsets);
+    return check_launch("k_slice_offsets");
 }
 
 }  // extern "C"

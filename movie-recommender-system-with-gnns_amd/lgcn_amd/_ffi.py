@@ -73,6 +73,9 @@ _SIGS = {
     "lgcn_score_filter": ([_vp, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp], ctypes.c_int),
     "lgcn_select_topk": ([_vp, _vp, _vp, _i32, _i32, _i32, _i64, _i64, _i64, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_legacy_choice": ([_vp, _vp, _i64, _i64, _i64, _vp], ctypes.c_int),
+    "lgcn_slice_schedule_workspace_size": ([_i64, _i64, _i32, _i32, _vp, _vp], ctypes.c_int),
+    "lgcn_slice_schedule_build": ([_vp, _vp, _i64, _i64, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _sz,
+                                   _vp], ctypes.c_int),
     "lgcn_flagged_rows_add": ([_vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _i64, _vp], ctypes.c_int),
     "lgcn_grad_norm_workspace_floats": ([], ctypes.c_int),
     "lgcn_grad_norm": ([_vp, _i32, _f32, _vp, _vp, _vp], ctypes.c_int),

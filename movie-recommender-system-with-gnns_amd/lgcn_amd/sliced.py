@@ -8,7 +8,8 @@ arithmetic as CPU scatter_add_ (and as the unsplit rows of the default schedule)
 Rows with a segment longer than ``chunk`` (hubs) are cut into chunks whose partials the combine
 pass adds after the last slice (as the default schedule does for its split rows).
 
-Built on the device from a direction's CSR with torch ops (once per edge set).
+Built on the device from a direction's CSR by lgcn_slice_schedule_build (csrc/lgcn_plan.hip),
+once per (edge set, width).
 """
 from __future__ import annotations
 
@@ -19,6 +20,7 @@ import torch
 from . import _ffi
 from .plan import CsrDirection
 
+MAX_SLICES = 250  # lgcn_slice_schedule_build keys carry the slice in 8 bits
 ITEM_FIRST = 0x20000000
 ITEM_LAST = 0x40000000
 
@@ -43,100 +45,51 @@ class SlicedDirection:
 
 def slice_bounds(N: int, U: int, d: int, slice_bytes: int) -> list[int]:
     """Boundaries over [0, N): the user range and the item range each cut into slices of about
-    slice_bytes of fp32 rows of width d."""
+    slice_bytes of fp32 rows of width d (at most MAX_SLICES in all)."""
     out = [0]
     U = min(max(int(U), 0), N)
     for lo, hi in ((0, U), (U, N)):
         n = hi - lo
         if n <= 0:
             continue
-        k = max(1, -(-n * d * 4 // slice_bytes))
+        k = min(MAX_SLICES // 2, max(1, -(-n * d * 4 // slice_bytes)))
         out += [lo + (n * i) // k for i in range(1, k)] + [hi]
     return sorted(set(out))
 
 
 def build_sliced(f: CsrDirection, N: int, bounds: list[int], chunk: int = 256) -> SlicedDirection | None:
-    """None when some row's neighbours are not in ascending order (an uncoalesced edge_index):
-    its slice segments would not be successive runs of its edge list, so the chain could not
-    follow CSR order — the plain schedule is used then."""
+    """The sliced schedule of direction f (lgcn_slice_schedule_build, on the device). None when
+    some row's neighbours are not in ascending order (an uncoalesced edge_index): its slice
+    segments would not be successive runs of its edge list, so the chain could not follow CSR
+    order — the plain schedule is used then."""
+    import ctypes
+
+    lib = _ffi.load()
     dev = f.rowptr.device
-    rowptr = f.rowptr
-    col = f.col.long()
-    E = col.numel()
+    E = f.col.numel()
     S = len(bounds) - 1
-    deg = rowptr[1:] - rowptr[:-1]
-    row = torch.repeat_interleave(torch.arange(N, device=dev), deg)
-    if E > 1 and bool(((col[1:] < col[:-1]) & (row[1:] == row[:-1])).any()):
+    stream = _ffi.stream_of(dev)
+    nbytes, cap = _ffi._sz(0), ctypes.c_int64(0)
+    _ffi.check(lib.lgcn_slice_schedule_workspace_size(E, N, S, chunk, ctypes.byref(nbytes), ctypes.byref(cap)),
+               "lgcn_slice_schedule_workspace_size")
+    ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=dev)
+    items = torch.empty((cap.value, 2), dtype=torch.int64, device=dev)
+    splits = torch.empty((max(N, 1), 4), dtype=torch.int32, device=dev)
+    offsets = torch.empty(S + 1, dtype=torch.int64, device=dev)
+    counts = torch.zeros(4, dtype=torch.int64, device=dev)
+    bnd = torch.tensor(bounds, dtype=torch.int64, device=dev)
+    _ffi.check(lib.lgcn_slice_schedule_build(f.rowptr.data_ptr(), _ffi.ptr(f.col), N, E, bnd.data_ptr(), S, chunk,
+                                             items.data_ptr(), cap.value, offsets.data_ptr(), splits.data_ptr(),
+                                             splits.shape[0], counts.data_ptr(), ws.data_ptr(), ws.numel(), stream),
+               "lgcn_slice_schedule_build")
+    host = torch.cat([counts, offsets]).cpu().tolist()  # one read-back per plan
+    n_items, n_splits, n_partials, unsorted = host[:4]
+    off = host[4:]
+    del ws
+    if unsorted:
         return None
-    bnd = torch.tensor(bounds[1:-1], dtype=torch.long, device=dev)
-    s_of = torch.bucketize(col, bnd, right=True)
-    start = torch.ones(E, dtype=torch.bool, device=dev)
-    if E > 1:
-        start[1:] = (row[1:] != row[:-1]) | (s_of[1:] != s_of[:-1])
-    seg_beg = torch.nonzero(start).squeeze(1)
-    nseg = seg_beg.numel()
-    seg_len = torch.diff(torch.cat([seg_beg, torch.tensor([E], device=dev)]))
-    seg_row = row[seg_beg]
-    seg_s = s_of[seg_beg]
-    # hub rows: any segment longer than chunk -> chunked partials + combine
-    hub = torch.zeros(N, dtype=torch.bool, device=dev)
-    hub[seg_row[seg_len > chunk]] = True
-    seg_hub = hub[seg_row]
-    # row items (non-hub segments), with FIRST / LAST flags
-    first_seg = torch.ones(nseg, dtype=torch.bool, device=dev)
-    last_seg = torch.ones(nseg, dtype=torch.bool, device=dev)
-    if nseg > 1:
-        first_seg[1:] = seg_row[1:] != seg_row[:-1]
-        last_seg[:-1] = seg_row[1:] != seg_row[:-1]
-    keep = ~seg_hub
-    r_beg, r_len, r_row, r_s = seg_beg[keep], seg_len[keep], seg_row[keep], seg_s[keep]
-    r_flags = torch.where(first_seg[keep], ITEM_FIRST, 0) | torch.where(last_seg[keep], ITEM_LAST, 0)
-    # empty non-hub rows: one flag-only item in slice 0 (its epilogue still runs)
-    empty = torch.nonzero(deg == 0).squeeze(1)
-    r_beg = torch.cat([r_beg, torch.zeros_like(empty)])
-    r_len = torch.cat([r_len, torch.zeros_like(empty)])
-    r_row = torch.cat([r_row, empty])
-    r_s = torch.cat([r_s, torch.zeros_like(empty)])
-    r_flags = torch.cat([r_flags, torch.full_like(empty, ITEM_FIRST | ITEM_LAST)])
-    r_word = (r_len | r_flags) | (r_row << 32)
-    # hub chunks: partial slots per hub row in CSR order
-    hseg = torch.nonzero(seg_hub).squeeze(1)
-    h_len = seg_len[hseg]
-    nch = (h_len + chunk - 1) // chunk
-    c_seg = torch.repeat_interleave(hseg, nch)
-    c_first = torch.cumsum(nch, 0) - nch
-    c_idx = torch.arange(c_seg.numel(), device=dev) - torch.repeat_interleave(c_first, nch)
-    c_beg = seg_beg[c_seg] + c_idx * chunk
-    c_len = torch.minimum(seg_len[c_seg] - c_idx * chunk, torch.tensor(chunk, device=dev))
-    c_row = seg_row[c_seg]
-    c_s = seg_s[c_seg]
-    hub_rows = torch.nonzero(hub).squeeze(1)
-    per_row = torch.bincount(c_row, minlength=N)
-    pbeg_row = torch.cumsum(per_row, 0) - per_row
-    # chunks are generated in CSR order, so rank within the row = position - first position
-    first_pos = torch.full((N,), -1, dtype=torch.long, device=dev)
-    pos = torch.arange(c_row.numel(), device=dev)
-    if c_row.numel():
-        first_pos.scatter_reduce_(0, c_row, pos, reduce="amin", include_self=False)
-    c_slot = pbeg_row[c_row] + (pos - first_pos[c_row])
-    c_word = (c_len & 0xFFFFFFFF) | ((-(c_slot) - 1) << 32)
-    n_partials = int(per_row.sum())
-    splits = torch.stack([hub_rows, pbeg_row[hub_rows], per_row[hub_rows], torch.zeros_like(hub_rows)], 1)
-    splits = splits.to(torch.int32).contiguous()
-    # per-slice launches, longest first
-    all_beg = torch.cat([r_beg, c_beg])
-    all_len = torch.cat([r_len, c_len])
-    all_word = torch.cat([r_word, c_word])
-    all_s = torch.cat([r_s, c_s])
-    order = torch.argsort(all_s * (1 << 32) + (chunk * 64 - torch.clamp(all_len, max=chunk * 64)), stable=True)
-    all_beg, all_word, all_s = all_beg[order], all_word[order], all_s[order]
-    counts = torch.bincount(all_s, minlength=S).tolist()
-    items = torch.stack([all_beg, all_word], 1).contiguous()
-    launches, o = [], 0
-    for c in counts:
-        launches.append((items[o:o + c], c))
-        o += c
-    return SlicedDirection(f, launches, splits, int(hub_rows.numel()), n_partials, list(bounds))
+    launches = [(items[off[s]:off[s + 1]], off[s + 1] - off[s]) for s in range(S)]
+    return SlicedDirection(f, launches, splits, n_splits, n_partials, list(bounds))
 
 
 def _tail(sd: SlicedDirection, N, d, x, e, acc, y, mode, div, mul, partial, stream):
