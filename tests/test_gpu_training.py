@@ -305,3 +305,31 @@ def test_lazy_train_step_matches_dense_step(gpu, use_graphs, clip):
         assert abs(a - b) <= 1e-5 * max(1.0, abs(a))
     for x, y in ((res[0][1], res[1][1]), (res[0][2], res[1][2])):
         assert (x - y).abs().max().item() <= 1e-3 * x.abs().max().item()
+
+
+def test_recall20_parity_after_training(gpu, cpu_negatives):
+    """BASELINE.json: Recall@20 within ±0.002 of the reference. The reference harness
+    (utils/train_test.py train + evaluate) trains the HIP model on the GPU and the oracle model
+    (PyG 2.4.0 LGConv restated, oracle/lgconv_torch.py) on the CPU for 5 epochs over the
+    golden Cluster-GCN batches, same negatives; then Recall@20 and Recall@100 on the golden
+    validation edges with the same numpy seed."""
+    from utils import train_test as TT
+
+    hip, ref = _models(gpu)
+    batches = [torch.from_numpy(G[f"train_batch{p}"]) for p in range(3)]
+    val = torch.from_numpy(G["val_edge_index"])
+    out = {}
+    for name, m, dev in (("hip", hip, gpu), ("ref", ref, torch.device("cpu"))):
+        opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+        cpu_negatives(21)
+        for _ in range(5):
+            TT.train(m, opt, [_Batch(x) for x in batches], dev)
+        with torch.no_grad():
+            embs = TT.compute_embeddings(m, _Batch(val).to(dev), dev)
+            rec = {}
+            for k in (20, 100):
+                np.random.seed(5)
+                rec[k] = TT.compute_recall_at_k((embs[1], embs[3], embs[5]), k=k)
+        out[name] = rec
+    for k in (20, 100):
+        assert abs(out["hip"][k] - out["ref"][k]) <= 0.002, (k, out)
