@@ -7,9 +7,10 @@ models/light_gcn.py:28-40) with the plan (CSR + gcn_norm + schedule) already bui
 embedding tables resident in HBM. value = K * E * (graphs processed) / wall time.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
-GPU, each rank propagates its own independent graph instance (seed = rank) — Cluster-GCN-style
-sharding of independent units, no data-path collective (scaling: weak). The barrier and the
-max-over-ranks time go over RCCL.
+GPU. C2 is replicas only (the full-graph SpMM does not split without a per-layer
+exchange): each rank propagates its own independent graph instance (seed = rank), no data-path
+collective (scaling: weak). C5 (--config c5) is feature-sharded: one graph, d/N columns per
+rank, no collective (scaling: strong). The barrier and the max-over-ranks time go over RCCL.
 
 Also reported (one JSON line on rank 0):
   roofline     — achieved algorithmic GB/s of the dominant kernel (the item pass, k_spmm_vec;
@@ -287,7 +288,7 @@ def main():
                    "chunk": plan.chunk, "graphs": 1 if c5 else world,
                    "parallelism": (f"feature-sharded over {world} GPU(s): {d} columns each, full plan per rank, "
                                    "no collective") if c5 else
-                                  f"{world} independent graph instance(s), one per GPU, no collective"},
+                                  f"replicas: {world} independent graph instance(s), one per GPU, no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": (f"k_spmm_vec<{kernel_lpr(d)},sliced> (lgcn_spmm_run, {n_slices} source-slice "
