@@ -175,6 +175,15 @@ int lgcn_spmm_combine(const lgcn_item_t* items, int64_t n_items,
                       float* acc_lo, float* acc_hi, int64_t acc_split,
                       float* partial, int32_t mode, float div, float mul,
                       lgcn_stream_t stream);
+/* to_undirected + coalesce (reference data/dataset_handler.py:141, PyG 2.4.0 semantics): the
+ * 2P keys row*N+col of both directions of the P pairs, sorted ascending and deduplicated into
+ * (out_row, out_col)[*out_count] (capacity 2P). Ids outside [0, N) are counted in *err_count
+ * (and clamped; the caller raises). */
+int lgcn_coalesce_workspace_size(int64_t P, int64_t N, size_t* bytes);
+int lgcn_coalesce_undirected(const int64_t* src, const int64_t* dst, int64_t P, int64_t N, int64_t* out_row,
+                             int64_t* out_col, int64_t* out_count, int64_t* err_count, void* ws, size_t ws_bytes,
+                             lgcn_stream_t stream);
+
 /* Source-sliced schedule (lgcn_amd/sliced.py): S slices of the source id range, bounds[0..S]
  * (device int64, bounds[0] = 0, bounds[S] = N, S <= 250). Every row's CSR run is cut where its
  * neighbour's slice changes; a row with a segment longer than chunk is a hub (its segments are

@@ -302,6 +302,54 @@ int64_t slice_items_cap(int64_t E, int64_t N, int S, int32_t chunk) {
     return segs + E / chunk + N + 1;
 }
 
+// ---- to_undirected / coalesce (reference data/dataset_handler.py:141, PyG 2.4.0) ----
+__global__ void k_pair_keys(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t P, int64_t N,
+                            unsigned long long* __restrict__ keys, int32_t* __restrict__ bad) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < P; i += stride) {
+        const int64_t a = src[i], b = dst[i];
+        if (a < 0 || a >= N || b < 0 || b >= N) atomicOr(bad, 1);
+        const int64_t ca = a < 0 ? 0 : (a >= N ? N - 1 : a);
+        const int64_t cb = b < 0 ? 0 : (b >= N ? N - 1 : b);
+        keys[i] = static_cast<unsigned long long>(ca) * static_cast<unsigned long long>(N) + static_cast<unsigned long long>(cb);
+        keys[P + i] = static_cast<unsigned long long>(cb) * static_cast<unsigned long long>(N) + static_cast<unsigned long long>(ca);
+    }
+}
+
+__global__ void k_unique_flags(const unsigned long long* __restrict__ k, int64_t n, int32_t* __restrict__ flag) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+        flag[i] = (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
+}
+
+__global__ void k_unique_scatter(const unsigned long long* __restrict__ k, const int32_t* __restrict__ flag,
+                                 const int32_t* __restrict__ pos, int64_t n, int64_t N, int64_t* __restrict__ row,
+                                 int64_t* __restrict__ col, int64_t* __restrict__ count) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (flag[i]) {
+            const unsigned long long v = k[i];
+            row[pos[i]] = static_cast<int64_t>(v / static_cast<unsigned long long>(N));
+            col[pos[i]] = static_cast<int64_t>(v % static_cast<unsigned long long>(N));
+        }
+        if (i == n - 1) count[0] = pos[i] + flag[i];
+    }
+}
+
+size_t coalesce_cub_bytes(int64_t n, int bits) {
+    size_t a = 0, b = 0;
+    (void)hipcub::DeviceRadixSort::SortKeys(nullptr, a, (const unsigned long long*)nullptr,
+                                            (unsigned long long*)nullptr, static_cast<int>(n), 0, bits);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr, static_cast<int>(n));
+    return a > b ? a : b;
+}
+
+int coalesce_bits(int64_t N) {
+    int b = 1;
+    while (b < 64 && (b >= 63 || (int64_t(1) << b) < N * N)) ++b;
+    return b;
+}
+
 // sizes of the cub temp storage we need
 size_t csr_cub_bytes(int64_t E, int64_t N) {
     size_t t = 0;
@@ -576,6 +624,60 @@ int lgcn_slice_schedule_build(const int64_t* rowptr, const int32_t* col, int64_t
     // offsets over the sorted keys; padding keys (0xFFFFFFFF) sort after every real slice
     k_slice_offsets<<<1, 256, 0, s>>>(k_out, cap, S, offsets);
     return check_launch("k_slice_offsets");
+}
+
+
+int lgcn_coalesce_workspace_size(int64_t P, int64_t N, size_t* bytes) {
+    if (!bytes || P < 0 || N < 0) return fail(LGCN_E_ARG, "lgcn_coalesce_workspace_size: bad args");
+    if (2 * P > INT32_MAX || N > (int64_t(1) << 31)) return fail(LGCN_E_UNSUPPORTED, "coalesce: sizes exceed int32");
+    const int64_t n = 2 * P > 0 ? 2 * P : 1;
+    Carver c{nullptr, 0};
+    c.take<unsigned long long>(n);
+    c.take<unsigned long long>(n);
+    c.take<int32_t>(n);
+    c.take<int32_t>(n);
+    c.take<int32_t>(1);
+    c.take<char>(coalesce_cub_bytes(n, coalesce_bits(N > 1 ? N : 2)));
+    *bytes = c.used + 256;
+    return LGCN_OK;
+}
+
+int lgcn_coalesce_undirected(const int64_t* src, const int64_t* dst, int64_t P, int64_t N, int64_t* out_row,
+                             int64_t* out_col, int64_t* out_count, int64_t* err_count, void* ws, size_t ws_bytes,
+                             lgcn_stream_t stream) {
+    if (P < 0 || N <= 0 || !out_count || !err_count || (P > 0 && (!src || !dst || !out_row || !out_col)))
+        return fail(LGCN_E_ARG, "lgcn_coalesce_undirected: bad args");
+    if (2 * P > INT32_MAX) return fail(LGCN_E_UNSUPPORTED, "coalesce: sizes exceed int32");
+    hipStream_t s = as_stream(stream);
+    if (int rc = check_hip(hipMemsetAsync(out_count, 0, sizeof(int64_t), s), "memset count")) return rc;
+    if (int rc = check_hip(hipMemsetAsync(err_count, 0, sizeof(int64_t), s), "memset err")) return rc;
+    if (P == 0) return LGCN_OK;
+    const int64_t n = 2 * P;
+    const int bits = coalesce_bits(N > 1 ? N : 2);
+    Carver c{static_cast<char*>(ws), ws_bytes};
+    auto* k_in = c.take<unsigned long long>(n);
+    auto* k_out = c.take<unsigned long long>(n);
+    int32_t* flag = c.take<int32_t>(n);
+    int32_t* pos = c.take<int32_t>(n);
+    c.take<int32_t>(1);
+    const size_t cub_bytes = coalesce_cub_bytes(n, bits);
+    void* cub_tmp = c.take<char>(cub_bytes);
+    if (!c.ok) return fail(LGCN_E_WORKSPACE, "lgcn_coalesce_undirected: workspace %zu < %zu", ws_bytes, c.used);
+    const unsigned g = grid_for(n, kBlock, 16384);
+    k_pair_keys<<<grid_for(P, kBlock, 16384), kBlock, 0, s>>>(src, dst, P, N, k_in,
+                                                              reinterpret_cast<int32_t*>(err_count));
+    if (int rc = check_launch("k_pair_keys")) return rc;
+    size_t t = cub_bytes;
+    if (int rc = check_hip(hipcub::DeviceRadixSort::SortKeys(cub_tmp, t, k_in, k_out, static_cast<int>(n), 0, bits, s),
+                           "SortKeys(coalesce)"))
+        return rc;
+    k_unique_flags<<<g, kBlock, 0, s>>>(k_out, n, flag);
+    if (int rc = check_launch("k_unique_flags")) return rc;
+    t = cub_bytes;
+    if (int rc = check_hip(hipcub::DeviceScan::ExclusiveSum(cub_tmp, t, flag, pos, static_cast<int>(n), s), "scan unique"))
+        return rc;
+    k_unique_scatter<<<g, kBlock, 0, s>>>(k_out, flag, pos, n, N, out_row, out_col, out_count);
+    return check_launch("k_unique_scatter");
 }
 
 }  // extern "C"

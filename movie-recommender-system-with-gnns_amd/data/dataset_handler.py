@@ -62,7 +62,12 @@ def download_and_extract_dataset() -> None:
 
 
 def to_undirected(edge_index: torch.Tensor, num_nodes: int) -> torch.Tensor:
-    """Both directions, coalesced: sorted by row * N + col, duplicates removed (PyG semantics)."""
+    """Both directions, coalesced: sorted by row * N + col, duplicates removed (PyG semantics).
+    On a ROCm device: the HIP coalesce (lgcn_amd.ingest); CPU tensors keep the host path."""
+    if edge_index.is_cuda:
+        from lgcn_amd.ingest import to_undirected as to_undirected_hip
+
+        return to_undirected_hip(edge_index, num_nodes)
     row, col = edge_index[0], edge_index[1]
     key = torch.cat([row * num_nodes + col, col * num_nodes + row])
     key = torch.unique(key, sorted=True)
@@ -121,7 +126,11 @@ class MovieLensDataHandler:
 
     def _preprocess(self, user_idx: np.ndarray, movie_idx: np.ndarray) -> None:
         edge_index = torch.from_numpy(np.vstack((user_idx, movie_idx))).long()
-        self.edge_index = to_undirected(edge_index, self.num_users + self.num_movies)
+        if self.device.type == "cuda":  # coalesce on the device (HIP radix sort), keep the result on the host
+            edge_index = to_undirected(edge_index.to(self.device), self.num_users + self.num_movies).cpu()
+        else:
+            edge_index = to_undirected(edge_index, self.num_users + self.num_movies)
+        self.edge_index = edge_index
 
     @property
     def num_nodes(self) -> int:

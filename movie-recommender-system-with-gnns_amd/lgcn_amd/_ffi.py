@@ -76,6 +76,8 @@ _SIGS = {
     "lgcn_slice_schedule_workspace_size": ([_i64, _i64, _i32, _i32, _vp, _vp], ctypes.c_int),
     "lgcn_slice_schedule_build": ([_vp, _vp, _i64, _i64, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _sz,
                                    _vp], ctypes.c_int),
+    "lgcn_coalesce_workspace_size": ([_i64, _i64, _vp], ctypes.c_int),
+    "lgcn_coalesce_undirected": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
     "lgcn_flagged_rows_add": ([_vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _i64, _vp], ctypes.c_int),
     "lgcn_grad_norm_workspace_floats": ([], ctypes.c_int),
     "lgcn_grad_norm": ([_vp, _i32, _f32, _vp, _vp, _vp], ctypes.c_int),
