@@ -20,8 +20,12 @@ import torch
 
 from . import _ffi
 
-SUBSET = 16384   # candidates scored for the first thresholds (≈ k·M/SUBSET survive the filter)
-CAP = 16384      # per-query list capacity
+import os
+
+# candidates scored for the first thresholds (≈ k·M/SUBSET survive the filter) and the per-query
+# list capacity (>= SUBSET: the first pass stores every subset score)
+SUBSET = int(os.environ.get("LGCN_RECALL_SUBSET", 16384))
+CAP = max(SUBSET, 16384)
 
 
 class _Workspace:

@@ -312,7 +312,11 @@ def test_recall20_parity_after_training(gpu, cpu_negatives):
     (utils/train_test.py train + evaluate) trains the HIP model on the GPU and the oracle model
     (PyG 2.4.0 LGConv restated, oracle/lgconv_torch.py) on the CPU for 5 epochs over the
     golden Cluster-GCN batches, same negatives; then Recall@20 and Recall@100 on the golden
-    validation edges with the same numpy seed."""
+    validation edges with the same numpy seed. The two trainings drift apart by fp32 rounding
+    (torch reductions in bpr_loss on GPU vs CPU) that Adam's sign-like steps amplify on
+    noise-level gradients, so Recall differs by a few hits (measured 0.0018 / 0.0013 at k=20 /
+    100); SURVEY §8d's relative 1e-3 does not hold end to end, the north star's ±0.002 does.
+    With identical embeddings the hit counts are exact (tests/test_gpu_recall.py)."""
     from utils import train_test as TT
 
     hip, ref = _models(gpu)
@@ -320,7 +324,7 @@ def test_recall20_parity_after_training(gpu, cpu_negatives):
     val = torch.from_numpy(G["val_edge_index"])
     out = {}
     for name, m, dev in (("hip", hip, gpu), ("ref", ref, torch.device("cpu"))):
-        opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)  # the reference's learning rate
         cpu_negatives(21)
         for _ in range(5):
             TT.train(m, opt, [_Batch(x) for x in batches], dev)
@@ -332,4 +336,4 @@ def test_recall20_parity_after_training(gpu, cpu_negatives):
                 rec[k] = TT.compute_recall_at_k((embs[1], embs[3], embs[5]), k=k)
         out[name] = rec
     for k in (20, 100):
-        assert abs(out["hip"][k] - out["ref"][k]) <= 0.002, (k, out)
+        assert abs(out["hip"][k] - out["ref"][k]) <= 0.002, (k, out)  # BASELINE.json north star
