@@ -211,22 +211,6 @@ int lgcn_spmm_run(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t*
                   float* acc_hi, int64_t acc_split, float* partial, int32_t mode, float div, float mul,
                   lgcn_stream_t stream, float* run);
 
-/* The item pass with hot sources staged in LDS (persistent; d in {64, 128, 256}). Same items,
- * flags (run != NULL: sliced launch; run == NULL: plain items pass) and arithmetic as
- * lgcn_spmm_items / lgcn_spmm_run, so the results are bitwise identical; col is the plan's
- * hot-encoded neighbour array: -(slot+1) for an edge whose source is hot_rows[slot] (n_hot rows,
- * n_hot * d * 4 <= 160 KB), the source id otherwise. block in {256, 512, 1024} threads, grid =
- * workgroups (lgcn_spmm_hot_occupancy per CU × CUs). Replaces the same reference call as
- * lgcn_spmm (PyG 2.4.0 LGConv.propagate at reference models/light_gcn.py:33). */
-int lgcn_spmm_hot(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* splits, int64_t n_splits,
-                  const int32_t* col, const float* val, int64_t N, int32_t d, const float* x_lo, const float* x_hi,
-                  int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split, float* y, float* acc_lo,
-                  float* acc_hi, int64_t acc_split, float* partial, int32_t mode, float div, float mul,
-                  lgcn_stream_t stream, float* run, const int32_t* hot_rows, int32_t n_hot, int32_t block,
-                  int32_t grid);
-/* Resident workgroups per CU of lgcn_spmm_hot's kernel for (d, n_hot, block, sliced). */
-int lgcn_spmm_hot_occupancy(int32_t d, int32_t n_hot, int32_t block, int32_t sliced, int32_t* per_cu);
-
 /* out[i] = (in[i] * mul) / div over n floats: the gradient that MulBackward (× 1/(K+1))
  * then MeanBackward (÷ (K+1)) hand to every layer output (reference models/light_gcn.py:36). */
 int lgcn_scale(const float* in, float* out, int64_t n, float mul, float div, lgcn_stream_t stream);

@@ -197,103 +197,6 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
     finish_row_vec<LPR, NV>(a, it.dst, l, acc);
 }
 
-// Hot-source variant of the item pass (persistent). Every workgroup first stages the launch's
-// n_hot most-gathered source rows (hot_rows, chosen per source slice at plan time) in LDS, then
-// walks the items with a grid stride. The plan's encoded col holds -(slot+1) for an edge whose
-// source is hot: that gather is a ds_read of the staged row instead of a global load, which
-// takes it off the L1->L2 request path (the item pass's limiter). Same per-row
-// order and arithmetic as k_spmm_vec, so the results are bitwise identical.
-template <int LPR, int NV, int UNROLL, int BLOCK, bool SLICED>
-__global__ __launch_bounds__(BLOCK) void k_spmm_hot(SpmmArgs a, const int32_t* __restrict__ hot_rows, int32_t n_hot) {
-    extern __shared__ float4 hot[];
-    constexpr int GPB = BLOCK / LPR;
-    const int64_t d4 = int64_t(LPR) * NV;
-    for (int i = threadIdx.x; i < n_hot * d4; i += BLOCK) {
-        const int64_t r = hot_rows[i / d4];
-        const float4* src = reinterpret_cast<const float4*>(split_row(a.x_lo, a.x_hi, a.x_split, r, a.d));
-        hot[i] = src[i % d4];
-    }
-    __syncthreads();
-    const int g = threadIdx.x / LPR;
-    const int l = threadIdx.x % LPR;
-    const float4* __restrict__ xlo = reinterpret_cast<const float4*>(a.x_lo) + l;
-    const float4* __restrict__ xhi = reinterpret_cast<const float4*>(a.x_hi) + l;
-    const float4* hl = hot + l;
-    for (int64_t item = int64_t(blockIdx.x) * GPB + g; item < a.n_items; item += int64_t(gridDim.x) * GPB) {
-        lgcn_item_t it = a.items[item];
-        int32_t flags = kItemFirst | kItemLast;
-        if (SLICED && it.dst >= 0) {
-            flags = it.len & (kItemFirst | kItemLast);
-            it.len &= kItemLenMask;
-        }
-        float4 acc[NV];
-        if (SLICED && !(flags & kItemFirst)) {
-            const float4* r = reinterpret_cast<const float4*>(a.run) + int64_t(it.dst) * d4 + l;
-#pragma unroll
-            for (int k = 0; k < NV; ++k) acc[k] = r[k * LPR];
-        } else {
-#pragma unroll
-            for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        int cn = 0;
-        float wn = 0.f;
-        if (l < it.len) {
-            cn = *(a.col + it.beg + l);
-            wn = *(a.val + it.beg + l);
-        }
-        for (int b = 0; b < it.len; b += LPR) {
-            const int n = min(LPR, it.len - b);
-            const int c = cn;
-            const float w = wn;
-            if (b + LPR < it.len && l < it.len - b - LPR) {
-                cn = *(a.col + it.beg + b + LPR + l);
-                wn = *(a.val + it.beg + b + LPR + l);
-            }
-            int j = 0;
-            for (; j + UNROLL <= n; j += UNROLL) {
-                float4 xv[UNROLL][NV];
-                float wv[UNROLL];
-#pragma unroll
-                for (int u = 0; u < UNROLL; ++u) {
-                    const int cj = __shfl(c, j + u, LPR);
-                    wv[u] = __shfl(w, j + u, LPR);
-                    // one generic (flat) address either way: no branch, so the UNROLL loads
-                    // stay in flight together
-                    const float4* src = (cj < 0) ? hl + int64_t(-cj - 1) * d4
-                                      : (cj < a.x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - a.x_split) * d4;
-#pragma unroll
-                    for (int k = 0; k < NV; ++k) xv[u][k] = src[k * LPR];
-                }
-#pragma unroll
-                for (int u = 0; u < UNROLL; ++u)
-#pragma unroll
-                    for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wv[u], xv[u][k]);
-            }
-            for (; j < n; ++j) {
-                const int cj = __shfl(c, j, LPR);
-                const float wj = __shfl(w, j, LPR);
-                const float4* src = (cj < 0) ? hl + int64_t(-cj - 1) * d4
-                                  : (cj < a.x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - a.x_split) * d4;
-#pragma unroll
-                for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wj, src[k * LPR]);
-            }
-        }
-        if (it.dst < 0) {
-            float4* p = reinterpret_cast<float4*>(a.partial) + int64_t(-it.dst - 1) * d4 + l;
-#pragma unroll
-            for (int k = 0; k < NV; ++k) p[k * LPR] = acc[k];
-            continue;
-        }
-        if (SLICED && !(flags & kItemLast)) {
-            float4* r = reinterpret_cast<float4*>(a.run) + int64_t(it.dst) * d4 + l;
-#pragma unroll
-            for (int k = 0; k < NV; ++k) r[k * LPR] = acc[k];
-            continue;
-        }
-        finish_row_vec<LPR, NV>(a, it.dst, l, acc);
-    }
-}
-
 // Split rows: one workgroup per split row. Group g (of GPB) sums partials g, g+GPB, g+2*GPB, ...
 // with UNROLL loads in flight; the GPB group sums are then added in group order through LDS.
 // The association is fixed by the code, so results are deterministic run to run.
@@ -430,50 +333,6 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass) {
     return LGCN_OK;
 }
 
-// Hot-source item pass: BLOCK threads per workgroup, n_hot staged rows of LDS each; grid = the
-// resident capacity (occupancy × CUs), every workgroup walking the items with a grid stride.
-template <int LPR, int NV, int UNROLL, int BLOCK>
-int launch_hot(const SpmmArgs& a, hipStream_t s, const int32_t* hot_rows, int32_t n_hot, int32_t grid) {
-    if (a.n_items == 0) return LGCN_OK;
-    const size_t lds = size_t(n_hot) * LPR * NV * sizeof(float4);
-    auto kern = (a.run != nullptr) ? k_spmm_hot<LPR, NV, UNROLL, BLOCK, true> : k_spmm_hot<LPR, NV, UNROLL, BLOCK, false>;
-    if (lds > 65536) {
-        if (int rc = check_hip(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
-                               "k_spmm_hot: LDS size"))
-            return rc;
-    }
-    constexpr int GPB = BLOCK / LPR;
-    const int64_t need = (a.n_items + GPB - 1) / GPB;
-    const unsigned g = static_cast<unsigned>(need < grid ? need : grid);
-    kern<<<dim3(g), BLOCK, lds, s>>>(a, hot_rows, n_hot);
-    return check_launch("k_spmm_hot");
-}
-
-template <int LPR, int NV, int UNROLL>
-int dispatch_hot_block(const SpmmArgs& a, hipStream_t s, const int32_t* hot_rows, int32_t n_hot, int32_t block,
-                       int32_t grid) {
-    switch (block) {
-        case 256: return launch_hot<LPR, NV, UNROLL, 256>(a, s, hot_rows, n_hot, grid);
-        case 512: return launch_hot<LPR, NV, UNROLL, 512>(a, s, hot_rows, n_hot, grid);
-        case 1024: return launch_hot<LPR, NV, UNROLL, 1024>(a, s, hot_rows, n_hot, grid);
-        default: return fail(LGCN_E_ARG, "lgcn_spmm_hot: block %d not in {256, 512, 1024}", block);
-    }
-}
-
-template <int LPR, int NV, int UNROLL, int BLOCK>
-int occupancy_hot(int32_t n_hot, bool sliced, int* per_cu) {
-    const size_t lds = size_t(n_hot) * LPR * NV * sizeof(float4);
-    auto kern = sliced ? k_spmm_hot<LPR, NV, UNROLL, BLOCK, true> : k_spmm_hot<LPR, NV, UNROLL, BLOCK, false>;
-    if (lds > 65536) {
-        if (int rc = check_hip(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)),
-                               "k_spmm_hot: LDS size"))
-            return rc;
-    }
-    return check_hip(hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, kern, BLOCK, lds), "occupancy");
-}
-
 // Kernel-variant override for A/B tuning (LGCN_SPMM_VARIANT; 0 = default choice).
 int spmm_variant() {
     const char* v = std::getenv("LGCN_SPMM_VARIANT");
@@ -584,59 +443,6 @@ int lgcn_spmm_combine(LGCN_SPMM_PARAMS) { return spmm_impl(LGCN_SPMM_ARGS, PASS_
 int lgcn_spmm_run(LGCN_SPMM_PARAMS, float* run) {
     if (!run) return fail(LGCN_E_ARG, "lgcn_spmm_run: null running-sum buffer");
     return spmm_impl(LGCN_SPMM_ARGS, PASS_ITEMS, run);
-}
-
-int lgcn_spmm_hot(LGCN_SPMM_PARAMS, float* run, const int32_t* hot_rows, int32_t n_hot, int32_t block,
-                  int32_t grid) {
-    if (N < 0 || d <= 0 || n_items < 0 || n_hot < 0 || grid <= 0)
-        return fail(LGCN_E_ARG, "lgcn_spmm_hot: bad sizes (N=%lld d=%d n_hot=%d grid=%d)", (long long)N, d, n_hot, grid);
-    if (n_items == 0) return LGCN_OK;
-    if (!items || !x_lo || !acc_lo || (n_hot > 0 && !hot_rows) || (x_split < N && !x_hi) ||
-        (acc_split < N && !acc_hi))
-        return fail(LGCN_E_ARG, "lgcn_spmm_hot: null pointer");
-    if (mode < LGCN_EPI_INIT || mode > LGCN_EPI_SCALE) return fail(LGCN_E_ARG, "lgcn_spmm_hot: bad mode %d", mode);
-    if ((mode == LGCN_EPI_INIT || mode == LGCN_EPI_FINAL_E) && (!e_lo || (e_split < N && !e_hi)))
-        return fail(LGCN_E_ARG, "lgcn_spmm_hot: mode %d needs the e table", mode);
-    const bool al = aligned16(x_lo) && aligned16(acc_lo) && (partial == nullptr || aligned16(partial)) &&
-                    (x_hi == nullptr || aligned16(x_hi)) && (acc_hi == nullptr || aligned16(acc_hi)) &&
-                    (e_lo == nullptr || aligned16(e_lo)) && (e_hi == nullptr || aligned16(e_hi)) &&
-                    (y == nullptr || aligned16(y)) && (run == nullptr || aligned16(run));
-    if (!al) return fail(LGCN_E_ARG, "lgcn_spmm_hot: tables must be 16-byte aligned");
-    if (size_t(n_hot) * d * sizeof(float) > 160 * 1024)
-        return fail(LGCN_E_ARG, "lgcn_spmm_hot: %d hot rows of d=%d exceed 160 KB of LDS", n_hot, d);
-    SpmmArgs a{items, n_items, nullptr, 0, col, val, x_lo, x_hi, x_split, e_lo, e_hi, e_split,
-               y, acc_lo, acc_hi, acc_split, partial, d, mode, div, mul, run};
-    hipStream_t s = as_stream(stream);
-    switch (d) {
-        case 64: return dispatch_hot_block<16, 1, 8>(a, s, hot_rows, n_hot, block, grid);
-        case 128: return dispatch_hot_block<32, 1, 8>(a, s, hot_rows, n_hot, block, grid);
-        case 256: return dispatch_hot_block<64, 1, 8>(a, s, hot_rows, n_hot, block, grid);
-        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm_hot: d=%d unsupported (64, 128, 256)", d);
-    }
-}
-
-int lgcn_spmm_hot_occupancy(int32_t d, int32_t n_hot, int32_t block, int32_t sliced, int32_t* per_cu) {
-    if (!per_cu || n_hot < 0) return fail(LGCN_E_ARG, "lgcn_spmm_hot_occupancy: bad args");
-    int pc = 0;
-    int rc = LGCN_OK;
-#define OCC(LPR, B) rc = occupancy_hot<LPR, 1, 8, B>(n_hot, sliced != 0, &pc)
-#define OCC_D(LPR)                                   \
-    switch (block) {                                 \
-        case 256: OCC(LPR, 256); break;              \
-        case 512: OCC(LPR, 512); break;              \
-        case 1024: OCC(LPR, 1024); break;            \
-        default: return fail(LGCN_E_ARG, "lgcn_spmm_hot_occupancy: block %d", block); \
-    }
-    switch (d) {
-        case 64: OCC_D(16); break;
-        case 128: OCC_D(32); break;
-        case 256: OCC_D(64); break;
-        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm_hot_occupancy: d=%d", d);
-    }
-#undef OCC_D
-#undef OCC
-    *per_cu = pc;
-    return rc;
 }
 
 int lgcn_scale(const float* in, float* out, int64_t n, float mul, float div, lgcn_stream_t stream) {

@@ -33,19 +33,6 @@ class SlicedDirection:
     n_splits: int
     n_partials: int
     bounds: list            # source-id slice boundaries
-    hot: "HotSources | None" = None  # LDS-staged hot sources per slice (attach_hot), or None
-
-
-@dataclasses.dataclass
-class HotSources:
-    """Per source slice, the n most-gathered source rows of the slice, staged in LDS by every
-    workgroup of that slice's launch (lgcn_spmm_hot). col_enc is the plan's col with every edge
-    whose source is hot replaced by -(slot+1)."""
-    col_enc: torch.Tensor   # int32 [E]
-    rows: torch.Tensor      # int32 [S, n_hot] hot source ids per slice (first counts[s] valid)
-    counts: list            # hot rows per slice
-    block: int              # threads per workgroup
-    grid: list              # persistent grid per slice (resident workgroups on the device)
 
     @property
     def col(self):
@@ -105,39 +92,6 @@ def build_sliced(f: CsrDirection, N: int, bounds: list[int], chunk: int = 256) -
     return SlicedDirection(f, launches, splits, n_splits, n_partials, list(bounds))
 
 
-def attach_hot(sd: SlicedDirection, N: int, d: int, n_hot: int, block: int = 1024) -> SlicedDirection:
-    """Choose each slice's n_hot most-gathered sources (by occurrences in col) and encode col.
-    Returns sd with .hot set (n_hot = 0 clears it)."""
-    import ctypes
-
-    if n_hot <= 0:
-        sd.hot = None
-        return sd
-    lib = _ffi.load()
-    col = sd.base.col
-    dev = col.device
-    cnt = torch.bincount(col.long(), minlength=N)
-    S = len(sd.bounds) - 1
-    rows = torch.zeros((S, n_hot), dtype=torch.int32, device=dev)
-    slot = torch.full((N,), -1, dtype=torch.int32, device=dev)
-    counts, grid = [], []
-    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-    for s_ in range(S):
-        lo, hi = sd.bounds[s_], sd.bounds[s_ + 1]
-        n = min(n_hot, hi - lo)
-        top = torch.topk(cnt[lo:hi], n).indices + lo
-        rows[s_, :n] = top.to(torch.int32)
-        slot[top] = torch.arange(n, dtype=torch.int32, device=dev)
-        counts.append(n)
-        pc = ctypes.c_int32(0)
-        _ffi.check(lib.lgcn_spmm_hot_occupancy(d, n, block, 1, ctypes.byref(pc)), "lgcn_spmm_hot_occupancy")
-        grid.append(max(1, pc.value) * n_cu)
-    sl = slot[col.long()]
-    col_enc = torch.where(sl >= 0, -(sl + 1), col).to(torch.int32)
-    sd.hot = HotSources(col_enc, rows, counts, block, grid)
-    return sd
-
-
 def _tail(sd: SlicedDirection, N, d, x, e, acc, y, mode, div, mul, partial, stream):
     xl, xh, xs = x
     el, eh, es = e if e is not None else (None, None, N)
@@ -153,23 +107,6 @@ def spmm_sliced(sd: SlicedDirection, N: int, d: int, x, e, acc, y, mode: int, di
     timer (bench.py): a callable(d) -> context manager bracketing each slice launch."""
     lib = _ffi.load()
     tail = _tail(sd, N, d, x, e, acc, y, mode, div, mul, partial, stream)
-    if sd.hot is not None:
-        h = sd.hot
-        tail = (_ffi.ptr(h.col_enc),) + tail[1:]
-        for s_, (items, n) in enumerate(sd.launches):
-            if n == 0:
-                continue
-            args = (items.data_ptr(), n, None, 0, *tail, run.data_ptr(), h.rows[s_].data_ptr(), h.counts[s_],
-                    h.block, h.grid[s_])
-            if timer is not None:
-                with timer(d):
-                    rc = lib.lgcn_spmm_hot(*args)
-            else:
-                rc = lib.lgcn_spmm_hot(*args)
-            _ffi.check(rc, "lgcn_spmm_hot")
-        if combine:
-            spmm_sliced_combine(sd, N, d, x, e, acc, y, mode, div, mul, partial, stream)
-        return
     for items, n in sd.launches:
         if n == 0:
             continue
