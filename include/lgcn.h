@@ -353,6 +353,25 @@ int lgcn_adam_step(const lgcn_adam_tensor_t* tensors, int32_t n, float one_minus
 int lgcn_adam_prologue(double* step, float lr, double beta1, double beta2, float* scalars, lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Row-sparse gradient exchange (lgcn_exchange.hip) for data-parallel Cluster-GCN training with
+ * the row-lazy Adam: replaces the dense all_reduce of both embedding gradients per step (the
+ * DP form of reference utils/train_test.py:92-96) by an all_gather of each rank's
+ * nonzero gradient rows.
+ *   lgcn_rows_pack: slot i < n_a + n_b holds the listed row (rows_a, then keys_b[j] + off_b,
+ *     filtered by first_b / skip_b as in lgcn_row_adam) -> ids[i] and rows[i, :] = g[row];
+ *     filtered and trailing slots (up to cap) get ids[i] = -1.
+ *   lgcn_rows_mark_first: first[i] = 1 iff ids[i] >= 0 is the lowest index holding that row;
+ *     claim int32[N] must hold INT32_MAX on entry and holds it again on exit.
+ *   lgcn_rows_accumulate: for r = 0..world-1 in order, over slots [r*cap, (r+1)*cap):
+ *     g[row] = first ? rows[i] : g[row] + rows[i]; then, if div > 0, g[row] /= div once per row. */
+int lgcn_rows_pack(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
+                   int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
+                   const uint8_t* skip_b, int64_t cap, int64_t* ids, float* rows, lgcn_stream_t stream);
+int lgcn_rows_mark_first(const int64_t* ids, int64_t n, int32_t* claim, uint8_t* first, lgcn_stream_t stream);
+int lgcn_rows_accumulate(const int64_t* ids, const float* rows, int64_t world, int64_t cap, const uint8_t* first,
+                         float* g_lo, float* g_hi, int64_t split, int32_t d, float div, lgcn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * Host-side (no GPU): balanced k-way node partition for Cluster-GCN batching, the METIS
  * replacement for PyG ClusterData (reference data/dataset_handler.py:273). Deterministic
  * restreaming Linear Deterministic Greedy over the undirected adjacency of (src[e], dst[e]);

@@ -1,0 +1,197 @@
+// Row-sparse gradient exchange for data-parallel Cluster-GCN training (C4) with the row-lazy
+// Adam. The reference's DP equivalent is one dense all_reduce of both embedding gradients per
+// step (the single-GPU step is reference utils/train_test.py:86-96). A batch step
+// writes a nonzero gradient only on its rows (touched rows + first-occurrence negatives), a few
+// % of N, so each rank ships just those rows:
+//
+//   lgcn_rows_pack        rank r: its listed rows -> ids[cap] (int64, -1 = empty) + rows[cap, d]
+//   (all_gather over RCCL of ids and rows: [W, cap] and [W, cap, d])
+//   lgcn_rows_mark_first  first[i] = entry i is the first occurrence of its row in the gathered
+//                         list (deterministic: lowest index wins; claim[N] int32 = INT32_MAX
+//                         between calls, restored on exit)
+//   lgcn_rows_accumulate  per rank r = 0..W-1 in order: g[row] = first ? row_r : g[row] + row_r;
+//                         then g[row] /= W on the first entries (div > 0)
+//
+// Every rank runs the same launches on the same gathered bytes, so the gradient rows, the clip
+// norm over the union (lgcn_row_grad_norm with first_b) and the row Adam update are bitwise the
+// same on every rank, and the replicas stay identical. The per-row sum is rank order
+// (g0 + g1) + g2 ..., then / W, which is what a dense sum-then-divide computes for W = 2
+// exactly (a + b == b + a).
+
+#include <climits>
+
+#include "lgcn_common.h"
+
+using namespace lgcn;
+
+namespace {
+
+template <class T>
+__device__ __forceinline__ T* trow(T* lo, T* hi, int64_t split, int64_t r, int64_t d) {
+    return r < split ? lo + r * d : hi + (r - split) * d;
+}
+
+// One LPR-lane group per slot of the packed list (rows_a then keys_b, as lgcn_row_adam's list).
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_rows_pack(const float* __restrict__ g_lo, const float* __restrict__ g_hi,
+                                                      int64_t split, int32_t d, const int32_t* __restrict__ rows_a,
+                                                      int64_t n_a, const int64_t* __restrict__ keys_b, int64_t n_b,
+                                                      int64_t off_b, const uint8_t* __restrict__ first_b,
+                                                      const uint8_t* __restrict__ skip_b, int64_t cap,
+                                                      int64_t* __restrict__ ids, float* __restrict__ rows) {
+    constexpr int GPB = kBlock / LPR;
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    const int64_t i = int64_t(blockIdx.x) * GPB + g;
+    if (i >= cap) return;
+    int64_t row = -1;
+    if (i < n_a) {
+        row = rows_a[i];
+    } else if (i < n_a + n_b) {
+        const int64_t j = i - n_a;
+        row = keys_b[j] + off_b;
+        if ((first_b && !first_b[j]) || (skip_b && skip_b[row])) row = -1;
+    }
+    if (l == 0) ids[i] = row;
+    if (row < 0) return;
+    const float4* src = reinterpret_cast<const float4*>(trow(g_lo, g_hi, split, row, int64_t(d))) + l;
+    float4* dst = reinterpret_cast<float4*>(rows + i * int64_t(d)) + l;
+#pragma unroll
+    for (int q = 0; q < NV; ++q) dst[q * LPR] = src[q * LPR];
+}
+
+__global__ void k_claim_min(const int64_t* __restrict__ ids, int64_t n, int32_t* __restrict__ claim) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t r = ids[i];
+    if (r >= 0) atomicMin(claim + r, static_cast<int32_t>(i));
+}
+
+__global__ void k_claim_read(const int64_t* __restrict__ ids, int64_t n, const int32_t* __restrict__ claim,
+                             uint8_t* __restrict__ first) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t r = ids[i];
+    first[i] = (r >= 0 && claim[r] == static_cast<int32_t>(i)) ? 1 : 0;
+}
+
+__global__ void k_claim_reset(const int64_t* __restrict__ ids, int64_t n, int32_t* __restrict__ claim) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t r = ids[i];
+    if (r >= 0) claim[r] = INT_MAX;
+}
+
+// mode 0: g[row] = first ? x : g[row] + x (one rank's slots: rows unique within them)
+// mode 1: g[row] = g[row] / div on first entries
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_rows_accumulate(const int64_t* __restrict__ ids,
+                                                            const float* __restrict__ rows, int64_t n,
+                                                            const uint8_t* __restrict__ first, float* g_lo,
+                                                            float* g_hi, int64_t split, int32_t d, int mode,
+                                                            float div) {
+    constexpr int GPB = kBlock / LPR;
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    const int64_t i = int64_t(blockIdx.x) * GPB + g;
+    if (i >= n) return;
+    const int64_t row = ids[i];
+    if (row < 0) return;
+    const bool f = first[i] != 0;
+    if (mode == 1 && !f) return;
+    float4* G = reinterpret_cast<float4*>(trow(g_lo, g_hi, split, row, int64_t(d))) + l;
+    if (mode == 1) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const float4 v = G[q * LPR];
+            G[q * LPR] = make_float4(v.x / div, v.y / div, v.z / div, v.w / div);
+        }
+        return;
+    }
+    const float4* X = reinterpret_cast<const float4*>(rows + i * int64_t(d)) + l;
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+        const float4 x = X[q * LPR];
+        if (f) {
+            G[q * LPR] = x;
+        } else {
+            const float4 v = G[q * LPR];
+            G[q * LPR] = make_float4(v.x + x.x, v.y + x.y, v.z + x.z, v.w + x.w);
+        }
+    }
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+#define LGCN_EX_DISPATCH(CALL, WHAT)                                              \
+    switch (d) {                                                                  \
+        case 16: CALL(4, 1); break;                                               \
+        case 32: CALL(8, 1); break;                                               \
+        case 64: CALL(16, 1); break;                                              \
+        case 128: CALL(32, 1); break;                                             \
+        case 256: CALL(64, 1); break;                                             \
+        case 512: CALL(64, 2); break;                                             \
+        default: return fail(LGCN_E_UNSUPPORTED, WHAT ": d=%d unsupported", d); \
+    }
+
+}  // namespace
+
+extern "C" {
+
+int lgcn_rows_pack(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
+                   int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
+                   const uint8_t* skip_b, int64_t cap, int64_t* ids, float* rows, lgcn_stream_t stream) {
+    if (!g_lo || !ids || !rows || n_a < 0 || n_b < 0 || cap < n_a + n_b || (n_a > 0 && !rows_a) ||
+        (n_b > 0 && !keys_b))
+        return fail(LGCN_E_ARG, "lgcn_rows_pack: bad args (n_a=%lld n_b=%lld cap=%lld)", (long long)n_a,
+                    (long long)n_b, (long long)cap);
+    if (!al16(g_lo) || (g_hi && !al16(g_hi)) || !al16(rows))
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_rows_pack: tables must be 16-byte aligned");
+    if (cap == 0) return LGCN_OK;
+    hipStream_t s = as_stream(stream);
+#define LGCN_PK(LP, NVV)                                                                                       \
+    k_rows_pack<LP, NVV><<<grid_for(cap * LP, kBlock, int64_t(1) << 30), kBlock, 0, s>>>(                       \
+        g_lo, g_hi, split, d, rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b, cap, ids, rows)
+    LGCN_EX_DISPATCH(LGCN_PK, "lgcn_rows_pack")
+#undef LGCN_PK
+    return check_launch("k_rows_pack");
+}
+
+int lgcn_rows_mark_first(const int64_t* ids, int64_t n, int32_t* claim, uint8_t* first, lgcn_stream_t stream) {
+    if (n < 0 || (n > 0 && (!ids || !claim || !first)) || n > INT_MAX)
+        return fail(LGCN_E_ARG, "lgcn_rows_mark_first: bad args (n=%lld)", (long long)n);
+    if (n == 0) return LGCN_OK;
+    hipStream_t s = as_stream(stream);
+    const unsigned grid = grid_for(n, kBlock, int64_t(1) << 30);
+    k_claim_min<<<grid, kBlock, 0, s>>>(ids, n, claim);
+    if (int rc = check_launch("k_claim_min")) return rc;
+    k_claim_read<<<grid, kBlock, 0, s>>>(ids, n, claim, first);
+    if (int rc = check_launch("k_claim_read")) return rc;
+    k_claim_reset<<<grid, kBlock, 0, s>>>(ids, n, claim);
+    return check_launch("k_claim_reset");
+}
+
+int lgcn_rows_accumulate(const int64_t* ids, const float* rows, int64_t world, int64_t cap, const uint8_t* first,
+                         float* g_lo, float* g_hi, int64_t split, int32_t d, float div, lgcn_stream_t stream) {
+    if (world < 1 || cap < 0 || !g_lo || (cap > 0 && (!ids || !rows || !first)))
+        return fail(LGCN_E_ARG, "lgcn_rows_accumulate: bad args");
+    if (!al16(g_lo) || (g_hi && !al16(g_hi)) || (rows && !al16(rows)))
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_rows_accumulate: tables must be 16-byte aligned");
+    if (cap == 0) return LGCN_OK;
+    hipStream_t s = as_stream(stream);
+    const int64_t dd = d;
+#define LGCN_AC(LP, NVV)                                                                                         \
+    for (int64_t r = 0; r < world; ++r) {                                                                        \
+        k_rows_accumulate<LP, NVV><<<grid_for(cap * LP, kBlock, int64_t(1) << 30), kBlock, 0, s>>>(                \
+            ids + r * cap, rows + r * cap * dd, cap, first + r * cap, g_lo, g_hi, split, d, 0, 1.0f);            \
+        if (int rc = check_launch("k_rows_accumulate")) return rc;                                               \
+    }                                                                                                            \
+    if (div > 0.f)                                                                                               \
+        k_rows_accumulate<LP, NVV><<<grid_for(world * cap * LP, kBlock, int64_t(1) << 30), kBlock, 0, s>>>(        \
+            ids, rows, world * cap, first, g_lo, g_hi, split, d, 1, div)
+    LGCN_EX_DISPATCH(LGCN_AC, "lgcn_rows_accumulate")
+#undef LGCN_AC
+    return check_launch("k_rows_accumulate");
+}
+
+}  // extern "C"

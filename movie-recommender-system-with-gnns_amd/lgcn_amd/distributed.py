@@ -8,6 +8,10 @@ BPR + backward locally, then the two dense embedding gradients ([U,d] and [I,d])
 with one all_reduce each and divided by W, and every rank applies the identical
 clip_grad_norm_(1) + Adam step, so the replicated tables stay bitwise identical.
 With W = 1 this is exactly the reference step.
+
+With the row-lazy optimizer (lgcn_amd.optim.RowLazyAdam) the dense all_reduce is replaced by
+RowExchange: only the rows a step can make nonzero travel (all_gather of packed rows), every
+rank sums them in rank order, and every rank updates exactly the union of the ranks' rows.
 """
 from __future__ import annotations
 
@@ -45,6 +49,58 @@ def allreduce_grads(params, world: int) -> None:
             p.grad = torch.zeros_like(p)
         dist.all_reduce(p.grad, op=dist.ReduceOp.SUM)
         p.grad.div_(world)
+
+
+def exchange_capacity(batches, num_users: int) -> int:
+    """Slots per rank for the row-sparse gradient exchange: the most rows any batch's step can
+    list (its touched rows plus one negative per (user, positive) triplet), agreed across ranks
+    (all_gather needs equal sizes)."""
+    cap = 0
+    for b in batches:
+        ei = b.edge_index
+        n_t = int(torch.unique(ei).numel())
+        B = int((ei[0] < num_users).sum())
+        cap = max(cap, n_t + B)
+    world, _ = world_info()
+    if world > 1:
+        t = torch.tensor([cap], dtype=torch.int64)
+        if dist.get_backend() == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        cap = int(t.item())
+    return cap
+
+
+class RowExchange:
+    """Row-sparse DP gradient exchange for the row-lazy optimizer (csrc/lgcn_exchange.hip).
+
+    Per step each rank packs its listed gradient rows (ids int64 [cap], rows [cap, d]); the
+    packs are all-gathered (RCCL over xGMI; gloo in tests) and every rank sums them per row in
+    rank order and divides by W, so the union's gradient rows — and the clip norm and Adam update
+    over them — are bitwise identical on every rank. Bytes per rank per step: cap * (4d + 8),
+    against 4d * N for the dense all_reduce (C4: ~17k rows of 512 B vs 113 MB)."""
+
+    def __init__(self, cap: int, N: int, d: int, device, world: int):
+        self.cap, self.N, self.d, self.world = int(cap), int(N), int(d), int(world)
+        self.ids = torch.full((self.cap,), -1, dtype=torch.int64, device=device)
+        self.rows = torch.zeros((self.cap, self.d), dtype=torch.float32, device=device)
+        self.ids_all = torch.full((self.world * self.cap,), -1, dtype=torch.int64, device=device)
+        self.rows_all = torch.zeros((self.world * self.cap, self.d), dtype=torch.float32, device=device)
+        self.first = torch.zeros(self.world * self.cap, dtype=torch.uint8, device=device)
+        self.claim = torch.full((self.N,), 2**31 - 1, dtype=torch.int32, device=device)
+
+    def gather(self) -> None:
+        """The collective (eager, between the step's two captured halves)."""
+        if self.world == 1:
+            self.ids_all.copy_(self.ids)
+            self.rows_all.copy_(self.rows)
+            return
+        if dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(self.ids_all, self.ids)
+            dist.all_gather_into_tensor(self.rows_all, self.rows)
+        else:
+            dist.all_gather(list(self.ids_all.view(self.world, self.cap).unbind(0)), self.ids)
+            dist.all_gather(list(self.rows_all.view(self.world, self.cap, self.d).unbind(0)), self.rows)
 
 
 def train_epoch(model, optimizer, batches, device, seed: int = 0, epoch: int = 0, loss_fn=None,

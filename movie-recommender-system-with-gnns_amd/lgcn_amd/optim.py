@@ -104,8 +104,10 @@ class RowLazyAdam:
     with the arithmetic and per-step constants of FusedAdam(capturable=True), so after flush()
     every row holds what FusedAdam would have produced; only the clip coefficient's last bits
     can differ (its norm sums the touched rows only — the other rows' gradient is 0 — in another
-    order). Driven by lgcn_amd.train_step.FusedTrainStep(lazy=True) on one GPU; parameters are
-    stale between steps until flush() (call it before reading them: evaluation, checkpoints)."""
+    order). Driven by lgcn_amd.train_step.FusedTrainStep(lazy=True) — on one GPU, or data
+    parallel with a lgcn_amd.distributed.RowExchange (every rank steps the union of the ranks'
+    rows); parameters are stale between steps until flush() (call it before reading them:
+    evaluation, checkpoints)."""
 
     def __init__(self, user_w: torch.Tensor, item_w: torch.Tensor, lr: float = 1e-3, betas=(0.9, 0.999),
                  eps: float = 1e-8, max_grad_norm: float | None = 1.0, max_steps: int = 1 << 24):
@@ -158,7 +160,7 @@ class RowLazyAdam:
         """Bring the listed rows (duplicates allowed) up to the completed step count."""
         self._row_adam(rows_a, keys_b, off_b, None, None, 0, None, 0)
 
-    def step_rows(self, rows_a: torch.Tensor, keys_b: torch.Tensor | None = None, off_b: int = 0,
+    def step_rows(self, rows_a: torch.Tensor | None, keys_b: torch.Tensor | None = None, off_b: int = 0,
                   first_b: torch.Tensor | None = None, skip_b: torch.Tensor | None = None) -> None:
         """One Adam step whose gradient (self.gu / self.gi) is zero outside the listed rows, which
         must be duplicate-free (first_b / skip_b filter list b): clip norm over them, then the
@@ -168,10 +170,10 @@ class RowLazyAdam:
         lib = _ffi.load()
         clip = None
         if self.max_grad_norm is not None:
-            na = rows_a.numel()
+            na = rows_a.numel() if rows_a is not None else 0
             nb = keys_b.numel() if keys_b is not None else 0
             _ffi.check(lib.lgcn_row_grad_norm(self.gu.data_ptr(), self.gi.data_ptr(), self.U, self.d,
-                                              rows_a.data_ptr(), na, _ffi.ptr(keys_b), nb, off_b, _ffi.ptr(first_b),
+                                              _ffi.ptr(rows_a), na, _ffi.ptr(keys_b), nb, off_b, _ffi.ptr(first_b),
                                               _ffi.ptr(skip_b), float(self.max_grad_norm), self.norm_ws.data_ptr(),
                                               self.last_norm.data_ptr(), _ffi.stream_of(self.device)),
                        "lgcn_row_grad_norm")

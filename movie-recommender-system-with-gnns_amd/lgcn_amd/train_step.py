@@ -90,11 +90,13 @@ class FusedTrainStep:
     compute_grads(batch) -> loss: sets user/item_embedding.weight.grad only."""
 
     def __init__(self, model, optimizer, bpr_coeff: float = 5e-3, world: int = 1, max_entries: int = 4096,
-                 graphs: bool = False, lazy: bool = False):
+                 graphs: bool = False, lazy: bool = False, exchange=None):
         """graphs=True: the first step of each batch runs eagerly, then the whole step (gradients
         and, at world == 1, the optimizer — which must be a capturable FusedAdam) is captured in a
         per-batch hipGraph and replayed from then on; negatives still come from the global CUDA
-        generator (graph-safe Philox offsets), so each replay draws new ones."""
+        generator (graph-safe Philox offsets), so each replay draws new ones.
+        exchange (lazy, data parallel): a lgcn_amd.distributed.RowExchange; the step is then two
+        captured halves around the eager all_gather of the packed gradient rows."""
         self.model = model
         self.optimizer = optimizer
         self.coeff = float(bpr_coeff)
@@ -102,11 +104,14 @@ class FusedTrainStep:
         self.max_entries = max_entries
         self.graphs = graphs
         self.lazy = lazy
+        self.exchange = exchange
         if lazy:
             from .optim import RowLazyAdam
 
-            if not isinstance(optimizer, RowLazyAdam) or world != 1:
-                raise ValueError("lazy=True needs a lgcn_amd.optim.RowLazyAdam and world == 1")
+            if not isinstance(optimizer, RowLazyAdam):
+                raise ValueError("lazy=True needs a lgcn_amd.optim.RowLazyAdam")
+            if world > 1 and exchange is None:
+                raise ValueError("lazy=True with world > 1 needs a lgcn_amd.distributed.RowExchange")
         elif graphs and world == 1 and not getattr(optimizer, "capturable", False):
             raise ValueError("graphs=True needs a capturable optimizer (lgcn_amd.optim.FusedAdam(capturable=True))")
         self._states: dict[int, tuple[weakref.ref, int, _BatchState]] = {}
@@ -187,7 +192,14 @@ class FusedTrainStep:
     def _step_lazy(self, st: _BatchState) -> torch.Tensor:
         """The whole batch step with the row-lazy optimizer: catch the batch's rows (touched rows
         and this step's negatives) up, forward, loss, gradient rows written only where the step
-        can make them nonzero, backward, clip + Adam on exactly those rows."""
+        can make them nonzero, backward, [row exchange], clip + Adam on exactly those rows."""
+        loss = self._lazy_grads(st)
+        if self.exchange is not None:
+            self.exchange.gather()
+        self._lazy_update(st)
+        return loss
+
+    def _lazy_grads(self, st: _BatchState) -> torch.Tensor:
         m = self.model
         opt = self.optimizer
         lib = _ffi.load()
@@ -228,10 +240,37 @@ class FusedTrainStep:
             _ffi.check(lib.lgcn_flagged_rows_add(st.neg.data_ptr(), B, U, st.c2buf.data_ptr(),
                                                  st.c2flag.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U,
                                                  stream), "lgcn_flagged_rows_add")
-            # rows with a possibly nonzero gradient, each once: touched rows, then negatives at
-            # their first occurrence that are not touched
-            opt.step_rows(st.touched_rows, st.neg, U, first_b=st.c2flag, skip_b=st.plan.touched)
+            ex = self.exchange
+            if ex is not None:
+                # this rank's rows with a possibly nonzero gradient -> the exchange slots
+                _ffi.check(lib.lgcn_rows_pack(gu.data_ptr(), gi.data_ptr(), U, d, st.touched_rows.data_ptr(),
+                                              st.touched_rows.numel(), st.neg.data_ptr(), B, U,
+                                              st.c2flag.data_ptr(), st.plan.touched.data_ptr(), ex.cap,
+                                              ex.ids.data_ptr(), ex.rows.data_ptr(), stream), "lgcn_rows_pack")
         return st.loss
+
+    def _lazy_update(self, st: _BatchState) -> None:
+        """Clip + Adam on the rows whose gradient can be nonzero: this rank's (touched rows, then
+        negatives at their first occurrence that are not touched), or with an exchange the union
+        of every rank's, summed in rank order and divided by W."""
+        opt = self.optimizer
+        ex = self.exchange
+        with torch.no_grad():
+            if ex is None:
+                opt.step_rows(st.touched_rows, st.neg, self.model.num_users, first_b=st.c2flag,
+                              skip_b=st.plan.touched)
+                return
+            lib = _ffi.load()
+            m = self.model
+            stream = _ffi.stream_of(ex.ids_all.device)
+            n = ex.world * ex.cap
+            _ffi.check(lib.lgcn_rows_mark_first(ex.ids_all.data_ptr(), n, ex.claim.data_ptr(), ex.first.data_ptr(),
+                                                stream), "lgcn_rows_mark_first")
+            _ffi.check(lib.lgcn_rows_accumulate(ex.ids_all.data_ptr(), ex.rows_all.data_ptr(), ex.world, ex.cap,
+                                                ex.first.data_ptr(), opt.gu.data_ptr(), opt.gi.data_ptr(),
+                                                m.num_users, m.dim_h, float(ex.world), stream),
+                       "lgcn_rows_accumulate")
+            opt.step_rows(None, ex.ids_all, 0, first_b=ex.first)
 
     def sync(self) -> None:
         """Make the parameters current (row-lazy optimizer: replay every deferred row)."""
@@ -265,16 +304,26 @@ class FusedTrainStep:
             if getattr(st, "graph", None) is None:
                 loss = self._step_lazy(st)  # real first step (warms allocations), then capture
                 torch.cuda.synchronize()
-                g = torch.cuda.CUDAGraph()
                 steps = self.optimizer.steps
-                with torch.cuda.graph(g):
-                    st.graph_loss = self._step_lazy(st)
+                g = torch.cuda.CUDAGraph()
+                if self.exchange is None:
+                    with torch.cuda.graph(g):
+                        st.graph_loss = self._step_lazy(st)
+                else:  # two halves: the all_gather between them runs eagerly
+                    with torch.cuda.graph(g):
+                        st.graph_loss = self._lazy_grads(st)
+                    st.graph_post = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(st.graph_post):
+                        self._lazy_update(st)
                 self.optimizer.steps = steps  # the capture ran no step
                 st.graph = g
                 return loss
             if self.optimizer.steps + 1 > self.optimizer.max_steps:
                 raise RuntimeError("RowLazyAdam: max_steps exceeded")
             st.graph.replay()
+            if self.exchange is not None:
+                self.exchange.gather()
+                st.graph_post.replay()
             self.optimizer.steps += 1
             return st.graph_loss
         if not self.graphs:

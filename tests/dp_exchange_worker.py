@@ -1,0 +1,72 @@
+"""One rank of the data-parallel training check in tests/test_gpu_exchange.py (started as a
+child process per rank; gloo over one GPU): trains the same Cluster-GCN batches three ways —
+dense FusedAdam after an all_reduce of both gradients, and the row-lazy Adam with the
+row-sparse exchange (eager and hipGraph-replayed) — and saves the final tables and losses.
+
+python tests/dp_exchange_worker.py RANK WORLD PORT OUT CLIP"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "movie-recommender-system-with-gnns_amd"), ROOT, os.path.join(ROOT, "tests")]
+
+
+class _Batch:
+    def __init__(self, ei):
+        self.edge_index = ei
+
+    def to(self, device):
+        return self
+
+
+def main():
+    rank, world, port, out, clip = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], float(sys.argv[5])
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = port
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    gpu = torch.device("cuda:0")
+    torch.cuda.set_device(gpu)
+
+    import graphs
+    from lgcn_amd import cluster as C
+    from lgcn_amd import distributed as D
+    from lgcn_amd.optim import FusedAdam, RowLazyAdam
+    from lgcn_amd.train_step import FusedTrainStep
+    from models.light_gcn import LightGCN
+
+    U, I, ei = graphs.subsampled(U=2000, I=1000, pairs=8000, seed=4)
+    part = C.partition_nodes(ei, U + I, 8)
+    batches = [_Batch(torch.from_numpy(x).to(gpu)) for x in C.intra_part_edges(ei, part, 8)]
+    share = D.rank_share(len(batches), world, rank, seed=0, epoch=0)
+    cap = D.exchange_capacity(batches, U)
+    res = {}
+    for name in ("dense", "lazy", "lazy_graphs"):
+        torch.manual_seed(0)
+        m = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
+        if name == "dense":
+            opt = FusedAdam(m.parameters(), lr=1e-2, max_grad_norm=clip, capturable=True)
+            step = FusedTrainStep(m, opt, world=world)
+        else:
+            opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-2,
+                              max_grad_norm=clip)
+            ex = D.RowExchange(cap, U + I, 64, gpu, world)
+            step = FusedTrainStep(m, opt, world=world, lazy=True, exchange=ex, graphs=(name == "lazy_graphs"))
+        losses = []
+        for i in range(12):
+            torch.cuda.manual_seed(100 + 10 * i + rank)  # per-rank negatives, same for every variant
+            losses.append(step.step(batches[share[i % len(share)]]).item())
+        step.sync()
+        torch.cuda.synchronize()
+        res[name] = {"losses": losses, "user": m.user_embedding.weight.detach().cpu(),
+                     "item": m.item_embedding.weight.detach().cpu()}
+    res["cap"] = cap
+    torch.save(res, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,178 @@
+"""Row-sparse gradient exchange for data-parallel training (csrc/lgcn_exchange.hip,
+lgcn_amd.distributed.RowExchange): the kernels against a sequential restatement, the W = 1
+exchange against the plain row-lazy step, and a 2-rank run (gloo, one GPU, one child process
+per rank) against the dense all_reduce + FusedAdam data-parallel step."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+class _Batch:
+    def __init__(self, ei):
+        self.edge_index = ei
+
+    def to(self, device):
+        return self
+
+
+def _pack(lib, g, U, d, rows_a, keys_b, first_b, skip_b, cap, gpu):
+    from lgcn_amd import _ffi
+
+    ids = torch.empty(cap, dtype=torch.int64, device=gpu)
+    rows = torch.empty((cap, d), dtype=torch.float32, device=gpu)
+    _ffi.check(lib.lgcn_rows_pack(g[:U].data_ptr(), g[U:].data_ptr(), U, d, rows_a.data_ptr(), rows_a.numel(),
+                                  keys_b.data_ptr(), keys_b.numel(), U, first_b.data_ptr(), skip_b.data_ptr(), cap,
+                                  ids.data_ptr(), rows.data_ptr(), _ffi.stream_of(gpu)), "lgcn_rows_pack")
+    return ids, rows
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_exchange_kernels_match_sequential_restatement(gpu, d):
+    """pack (3 ranks' lists with duplicates, filters, padding) -> mark_first -> accumulate(/3),
+    bitwise against: for each slot in rank order, first occurrence stores, later ones add, /3."""
+    from lgcn_amd import _ffi
+
+    lib = _ffi.load()
+    U, I, W, cap = 500, 300, 3, 260
+    N = U + I
+    rng = np.random.default_rng(d)
+    gens = [torch.randn(N, d, device=gpu) for _ in range(W)]
+    ids_all, rows_all, expect_ids = [], [], []
+    for r in range(W):
+        rows_a = np.unique(rng.integers(0, N, 90)).astype(np.int32)
+        negs = rng.integers(0, I, 120)
+        first = np.zeros(len(negs), np.uint8)
+        first[np.unique(negs, return_index=True)[1]] = 1
+        skip = np.zeros(N, np.uint8)
+        skip[rows_a] = 1
+        ids, rows = _pack(lib, gens[r], U, d, torch.from_numpy(rows_a).to(gpu), torch.from_numpy(negs).to(gpu),
+                          torch.from_numpy(first).to(gpu), torch.from_numpy(skip).to(gpu), cap, gpu)
+        want = np.full(cap, -1, np.int64)
+        want[:len(rows_a)] = rows_a
+        for j, k in enumerate(negs):
+            if first[j] and not skip[k + U]:
+                want[len(rows_a) + j] = k + U
+        assert np.array_equal(ids.cpu().numpy(), want)
+        ok = torch.from_numpy(want >= 0).to(gpu)
+        assert torch.equal(rows[ok], gens[r][ids[ok]])
+        ids_all.append(ids)
+        rows_all.append(rows)
+    ids_all = torch.cat(ids_all)
+    rows_all = torch.cat(rows_all)
+    claim = torch.full((N,), 2**31 - 1, dtype=torch.int32, device=gpu)
+    first = torch.empty(W * cap, dtype=torch.uint8, device=gpu)
+    s = _ffi.stream_of(gpu)
+    _ffi.check(lib.lgcn_rows_mark_first(ids_all.data_ptr(), W * cap, claim.data_ptr(), first.data_ptr(), s), "mf")
+    assert torch.equal(claim, torch.full_like(claim, 2**31 - 1))
+    g = torch.full((N, d), float("nan"), device=gpu)  # rows outside the union must stay untouched
+    _ffi.check(lib.lgcn_rows_accumulate(ids_all.data_ptr(), rows_all.data_ptr(), W, cap, first.data_ptr(),
+                                        g[:U].data_ptr(), g[U:].data_ptr(), U, d, float(W), s), "acc")
+    ids_h = ids_all.cpu().numpy()
+    rows_h = rows_all.cpu()
+    ref = {}
+    seen = set()
+    first_ref = np.zeros(W * cap, np.uint8)
+    for i, r in enumerate(ids_h):
+        if r < 0:
+            continue
+        if r not in seen:
+            seen.add(r)
+            first_ref[i] = 1
+            ref[r] = rows_h[i].clone()
+        else:
+            ref[r] = ref[r] + rows_h[i]
+    assert np.array_equal(first.cpu().numpy(), first_ref)
+    gh = g.cpu()
+    for r, v in ref.items():
+        assert torch.equal(gh[r], v / W), r
+    outside = np.setdiff1d(np.arange(N), np.array(sorted(seen)))
+    assert torch.isnan(gh[outside]).all()
+
+
+@pytest.mark.parametrize("use_graphs", [False, True])
+def test_exchange_world1_equals_plain_lazy_step(gpu, use_graphs):
+    """With one rank the exchange must be a no-op: bitwise the plain row-lazy step."""
+    import graphs
+    from lgcn_amd import cluster as C
+    from lgcn_amd import distributed as D
+    from lgcn_amd.optim import RowLazyAdam
+    from lgcn_amd.train_step import FusedTrainStep
+    from models.light_gcn import LightGCN
+
+    U, I, ei = graphs.subsampled(U=2000, I=1000, pairs=8000, seed=4)
+    part = C.partition_nodes(ei, U + I, 8)
+    batches = [_Batch(torch.from_numpy(x).to(gpu)) for x in C.intra_part_edges(ei, part, 8)]
+    cap = D.exchange_capacity(batches, U)
+    res = []
+    for with_ex in (False, True):
+        torch.manual_seed(0)
+        m = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
+        opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-2, max_grad_norm=1.0)
+        ex = D.RowExchange(cap, U + I, 64, gpu, 1) if with_ex else None
+        step = FusedTrainStep(m, opt, graphs=use_graphs, lazy=True, exchange=ex)
+        losses = []
+        for i in range(12):
+            torch.cuda.manual_seed(100 + i)
+            losses.append(step.step(batches[i % 8]).item())
+        step.sync()
+        res.append((losses, m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("clip", [float("inf"), 1.0])
+def test_dp2_row_exchange_matches_dense_allreduce(gpu, tmp_path, clip):
+    """Two ranks (gloo, one GPU): the row-lazy step with the row-sparse exchange (eager and
+    hipGraph) vs dense all_reduce + FusedAdam on the same batches and negatives. Without
+    clipping: bitwise (W = 2: (a + b) / 2 either way). With clip 1: the norms sum the same
+    squares in another order (see test_lazy_train_step_matches_dense_step) — losses to 1e-5,
+    parameters to 1e-3 of their scale. Both ranks end bitwise identical in every variant."""
+    port = str(_free_port())
+    worker = str(ROOT / "tests" / "dp_exchange_worker.py")
+    outs = [str(tmp_path / f"r{r}.pt") for r in range(2)]
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
+    procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), "2", port, outs[r], str(clip)], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=100)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log
+    res = [torch.load(o, weights_only=True) for o in outs]
+    for name in ("dense", "lazy", "lazy_graphs"):
+        assert torch.equal(res[0][name]["user"], res[1][name]["user"]), name
+        assert torch.equal(res[0][name]["item"], res[1][name]["item"]), name
+    for r in range(2):
+        d, lz, lg = res[r]["dense"], res[r]["lazy"], res[r]["lazy_graphs"]
+        assert lz["losses"] == lg["losses"]
+        assert torch.equal(lz["user"], lg["user"]) and torch.equal(lz["item"], lg["item"])
+        if clip == float("inf"):
+            assert d["losses"] == lz["losses"]
+            assert torch.equal(d["user"], lz["user"]) and torch.equal(d["item"], lz["item"])
+        else:
+            for a, b in zip(d["losses"], lz["losses"]):
+                assert abs(a - b) <= 1e-5 * max(1.0, abs(a))
+            for k in ("user", "item"):
+                assert (d[k] - lz[k]).abs().max().item() <= 1e-3 * d[k].abs().max().item()
