@@ -152,6 +152,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for runs; gloo to rehearse N ranks on one GPU")
     ap.add_argument("--torch-adam", action="store_true", help="train: torch Adam + clip_grad_norm_ (reference ops)")
     ap.add_argument("--no-graphs", action="store_true", help="train: run the fused step eagerly (no hipGraph replay)")
+    ap.add_argument("--exchange", action="store_true",
+                    help="train, N=1: run the row exchange anyway (measures its kernels; N>1 always uses it)")
     ap.add_argument("--dense-adam", action="store_true",
                     help="train: dense FusedAdam over all rows every step instead of the row-lazy exact Adam")
     ap.add_argument("--autograd", action="store_true",
@@ -312,7 +314,8 @@ def run_train(args):
     graph: 90/5/5 directed split, train graph cut into --parts parts by the host LDG partitioner,
     --parts-per-batch parts per step (union of intra-part edges), BPR loss, backward through the
     HIP propagation, clip_grad_norm_(1), Adam(1e-3). N ranks = data parallel: disjoint batches per
-    rank, RCCL all_reduce of the two dense embedding gradients each step (lgcn_amd.distributed).
+    rank; with the default row-lazy Adam the ranks all_gather only their nonzero gradient rows
+    (lgcn_amd.distributed.RowExchange); --dense-adam all_reduces both dense gradient tables.
     value = K * (batch edges summed over ranks) / wall time."""
     import numpy as np
     import torch
@@ -354,7 +357,7 @@ def run_train(args):
         f"({time.perf_counter() - t0:.1f} s)")
     torch.manual_seed(0)
     model = LightGCN(U, I, num_layers=K, dim_h=d).to(dev)
-    lazy = not (args.autograd or args.torch_adam or args.dense_adam) and world == 1
+    lazy = not (args.autograd or args.torch_adam or args.dense_adam)
     if args.torch_adam:
         opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     elif lazy:
@@ -371,11 +374,18 @@ def run_train(args):
     torch.manual_seed(1000 + rank)
 
     fused = None
+    exchange = None
+    if lazy and (world > 1 or args.exchange):
+        # row-sparse DP gradient exchange: all_gather of each rank's nonzero gradient rows
+        cap = D.exchange_capacity(batches, U)
+        exchange = D.RowExchange(cap, N, d, dev, world)
+        log(f"[rank {rank}] row exchange: {cap} slots per rank, {cap * (4 * d + 8) / 1e6:.1f} MB sent per step "
+            f"(dense all_reduce: {N * d * 4 / 1e6:.1f} MB)")
     if not args.autograd:
         from lgcn_amd.train_step import FusedTrainStep
 
         fused = FusedTrainStep(model, opt, world=world, graphs=not args.no_graphs and not args.torch_adam,
-                               lazy=lazy)
+                               lazy=lazy, exchange=exchange)
 
     def step(bidx):
         batch = batches[bidx]
@@ -433,7 +443,10 @@ def run_train(args):
                            ("fused sparse step" + ("" if (args.no_graphs or args.torch_adam) else ", hipGraph per batch")),
                    "parts_per_batch": q, "f_intra": f_intra, "layers": K, "dim": d, "num_users": U,
                    "num_items": I, "train_edges": n_tr,
-                   "parallelism": f"dp{world}: disjoint part batches per rank, RCCL all_reduce of embedding grads"},
+                   "parallelism": (f"dp{world}: disjoint part batches per rank, " +
+                                   ("row-sparse gradient exchange (all_gather of each rank's nonzero rows), "
+                                    "row-lazy Adam on the union" if exchange is not None else
+                                    "RCCL all_reduce of embedding grads" if world > 1 else "single GPU"))},
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
