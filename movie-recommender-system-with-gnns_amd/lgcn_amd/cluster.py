@@ -18,7 +18,7 @@ import numpy as np
 from . import _ffi
 
 
-def partition_nodes(edge_index, num_nodes: int, num_parts: int, passes: int = 4,
+def partition_nodes(edge_index, num_nodes: int, num_parts: int, passes: int = 8,
                     imbalance: float = 0.05) -> np.ndarray:
     """part[N] in [0, num_parts): deterministic, balanced on node count. Host-only."""
     ei = np.ascontiguousarray(np.asarray(edge_index if not hasattr(edge_index, "cpu") else edge_index.cpu()),

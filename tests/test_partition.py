@@ -66,3 +66,16 @@ def test_empty_and_tiny():
     part = cluster.partition_nodes(np.zeros((2, 0), np.int64), 5, 3)
     assert sorted(cluster.part_sizes(part, 3).tolist()) == [1, 2, 2]
     assert cluster.intra_fraction(np.zeros((2, 0), np.int64), part) == 1.0
+
+
+def test_partition_recovers_planted_bipartite_communities():
+    """Refined partition (LDG passes + size-constrained label propagation + min-loss balance
+    fix-up) keeps >= 0.9 of the ground truth's intra-part edges on a planted user-item graph;
+    measured 0.757 vs 0.778 (tools/partition_quality.py has the larger case: 0.756 vs 0.781;
+    plain 4-pass LDG with the old fix-up reached 0.655 there)."""
+    g, truth = synth.planted_bipartite(8000, 3200, 64, seed=1)
+    part = cluster.partition_nodes(g.edge_index, g.num_nodes, 64)
+    sizes = cluster.part_sizes(part, 64)
+    assert sizes.max() - sizes.min() <= 1
+    q, t = cluster.intra_fraction(g.edge_index, part), cluster.intra_fraction(g.edge_index, truth)
+    assert q >= 0.9 * t, (q, t)
