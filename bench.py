@@ -108,7 +108,7 @@ def cpu_baseline(graph, K, d, seconds_budget=20.0):
     import numpy as np
     import torch
 
-    from oracle.lgconv_torch import time_reference_forward
+    from oracle.lgconv_torch import time_csr_forward, time_reference_forward
 
     threads = min(16, len(os.sched_getaffinity(0)))
     torch.set_num_threads(threads)
@@ -127,7 +127,21 @@ def cpu_baseline(graph, K, d, seconds_budget=20.0):
         t = time_reference_forward(uw, iw, ei, K, reps=reps)
     log(f"cpu_baseline: {ei.shape[1]} edges, {threads} threads, {t:.3f} s/forward "
         f"({time.perf_counter() - t0:.1f} s total)")
-    return {"value": K * ei.shape[1] / t, "unit": "edges/s", "cores": threads, "kind": "port",
+    # second CPU baseline: the whole C2 graph as one CSR matrix, torch.sparse.mm per layer
+    full = torch.from_numpy(graph.edge_index)
+    t1 = time.perf_counter()
+    tc = time_csr_forward(uw, iw, full, K, reps=3)
+    log(f"cpu_baseline csr: {full.shape[1]} edges, {tc:.3f} s/forward ({time.perf_counter() - t1:.1f} s total)")
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next(line.split(":", 1)[1].strip() for line in f if line.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    return {"value": K * ei.shape[1] / t, "unit": "edges/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "csr_spmm": {"value": K * full.shape[1] / tc, "unit": "edges/s", "cores": threads,
+                         "sample": f"all {full.shape[1]} C2 edges, K={K} d={d}: gcn_norm-weighted CSR built once, "
+                                   f"torch.sparse.mm per layer + layer mean, median of 3"},
             "sample": f"random {frac:.0%} of the C2 edges ({ei.shape[1]} edges, all {graph.num_nodes} nodes), "
                       f"K={K} d={d} forward: index_select -> mul -> scatter_add_ with gcn_norm per layer "
                       f"(PyG 2.4.0 LGConv op sequence, torch {torch.__version__} CPU), median of {reps}"}

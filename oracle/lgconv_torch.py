@@ -102,3 +102,32 @@ def time_reference_forward(user_w: torch.Tensor, item_w: torch.Tensor, edge_inde
             times.append(time.perf_counter() - t0)
     times = sorted(times[1:])
     return times[len(times) // 2]
+
+
+def time_csr_forward(user_w: torch.Tensor, item_w: torch.Tensor, edge_index: torch.Tensor, K: int,
+                     reps: int = 3) -> float:
+    """Median seconds of a K-layer forward with the "torch_sparse-style" CPU SpMM: the same
+    gcn_norm-weighted adjacency as one CSR matrix (built once, outside the timing, as
+    torch_sparse's SparseTensor would be), then y = torch.sparse.mm(A, x) per layer and the
+    layer-stack mean (BASELINE.md §3's second CPU baseline)."""
+    import time
+
+    N = user_w.shape[0] + item_w.shape[0]
+    w = gcn_norm_torch(edge_index, N)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", UserWarning)  # "sparse CSR support is in beta"
+        A = torch.sparse_coo_tensor(torch.stack([edge_index[1], edge_index[0]]), w, (N, N)).coalesce().to_sparse_csr()
+    times = []
+    with torch.no_grad():
+        for _ in range(reps + 1):
+            t0 = time.perf_counter()
+            emb = torch.cat([user_w, item_w])
+            acc = emb.clone()
+            for _ in range(K):
+                emb = torch.sparse.mm(A, emb)
+                acc += emb
+            out = acc / (K + 1) * (1 / (K + 1))
+            torch.split(out, [user_w.shape[0], item_w.shape[0]])
+            times.append(time.perf_counter() - t0)
+    times = sorted(times[1:])
+    return times[len(times) // 2]
