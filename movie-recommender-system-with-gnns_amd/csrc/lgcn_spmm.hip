@@ -118,7 +118,7 @@ __device__ __forceinline__ void finish_row_vec(const SpmmArgs& a, int64_t r, int
 // SLICED: one launch of a source-sliced schedule (lgcn_spmm_run). A row item continues the row's
 // running sum from a.run unless it is the row's FIRST segment, and runs the epilogue only on its
 // LAST one; the sum stays one sequential chain in CSR order across launches.
-template <int LPR, int NV, int UNROLL, bool SLICED = false>
+template <int LPR, int NV, int UNROLL, bool SLICED = false, int TAIL = 0>
 __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
     constexpr int GPB = kBlock / LPR;
     const int g = threadIdx.x / LPR;
@@ -173,6 +173,31 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
             for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
                 for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wv[u], xv[u][k]);
+        }
+        if (TAIL == 1 && j < n) {
+            // the batch's last n - j (< UNROLL) edges: all their gathers issued (exec-predicated)
+            // before the first add, then added in CSR order — one memory latency instead of n - j
+            const int rem = n - j;
+            float4 xv[UNROLL - 1][NV];
+            float wv[UNROLL - 1];
+#pragma unroll
+            for (int u = 0; u < UNROLL - 1; ++u) {
+                const int ju = j + (u < rem ? u : 0);
+                const int cj = __shfl(c, ju, LPR);
+                wv[u] = __shfl(w, ju, LPR);
+                const float4* src = (cj < a.x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - a.x_split) * d4;
+                if (u < rem) {
+#pragma unroll
+                    for (int k = 0; k < NV; ++k) xv[u][k] = src[k * LPR];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL - 1; ++u)
+                if (u < rem) {
+#pragma unroll
+                    for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wv[u], xv[u][k]);
+                }
+            j = n;
         }
         for (; j < n; ++j) {
             const int cj = __shfl(c, j, LPR);
@@ -315,15 +340,15 @@ __global__ __launch_bounds__(kBlock) void k_combine_scalar(SpmmArgs a) {
 
 enum { PASS_ITEMS = 1, PASS_COMBINE = 2, PASS_BOTH = 3 };
 
-template <int LPR, int NV, int UNROLL>
+template <int LPR, int NV, int UNROLL, int TAIL = 0>
 int launch_vec(const SpmmArgs& a, hipStream_t s, int pass) {
     constexpr int GPB = kBlock / LPR;
     if ((pass & PASS_ITEMS) && a.n_items > 0) {
         const int64_t blocks = (a.n_items + GPB - 1) / GPB;
         if (a.run != nullptr)
-            k_spmm_vec<LPR, NV, UNROLL, true><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+            k_spmm_vec<LPR, NV, UNROLL, true, TAIL><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
         else
-            k_spmm_vec<LPR, NV, UNROLL><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+            k_spmm_vec<LPR, NV, UNROLL, false, TAIL><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
         if (int rc = check_launch("k_spmm_vec")) return rc;
     }
     if ((pass & PASS_COMBINE) && a.n_splits > 0) {
@@ -403,14 +428,34 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
                   (e_lo == nullptr || aligned16(e_lo)) && (e_hi == nullptr || aligned16(e_hi)) &&
                   (y == nullptr || aligned16(y));
     if (vec_ok) {
+        // Predicated tail (TAIL = 1): a row's last < UNROLL edges of each batch are gathered
+        // together instead of one at a time. It costs VGPRs (occupancy 6-7 -> 4 waves/SIMD at
+        // d >= 32), so it is on where latency, not loads in flight, bounds the pass: d <= 64, and
+        // small plain-schedule launches (Cluster-GCN batch plans). Measured (profiles/r01k_tail/):
+        // C2 d=32 -6 %, d=64 -2 %, C3 training step -5 %; C2 d=128 / d=256 +3 % (kept off there).
+        // LGCN_SPMM_VARIANT (A/B knob): 1 = 16-deep unroll at d=64, 2 = tail on, 3 = tail off.
+        const int v = spmm_variant();
+        const bool tail = v == 2 || (v != 1 && v != 3 && (d <= 64 || (run == nullptr && n_items <= 65536)));
+        if (tail) {
+            switch (d) {
+                case 4: return launch_vec<1, 1, 8, 1>(a, s, pass);
+                case 8: return launch_vec<2, 1, 8, 1>(a, s, pass);
+                case 16: return launch_vec<4, 1, 8, 1>(a, s, pass);
+                case 32: return launch_vec<8, 1, 8, 1>(a, s, pass);
+                case 64: return launch_vec<16, 1, 8, 1>(a, s, pass);
+                case 128: return launch_vec<32, 1, 8, 1>(a, s, pass);
+                case 256: return launch_vec<64, 1, 8, 1>(a, s, pass);
+                case 512: return launch_vec<64, 2, 4, 1>(a, s, pass);
+                case 1024: return launch_vec<64, 4, 2, 1>(a, s, pass);
+                default: break;
+            }
+        }
         switch (d) {
             case 4: return launch_vec<1, 1, 8>(a, s, pass);
             case 8: return launch_vec<2, 1, 8>(a, s, pass);
             case 16: return launch_vec<4, 1, 8>(a, s, pass);
             case 32: return launch_vec<8, 1, 8>(a, s, pass);
-            case 64:
-                // A/B knob kept for tuning: 1 = 16-deep gather unroll
-                return spmm_variant() == 1 ? launch_vec<16, 1, 16>(a, s, pass) : launch_vec<16, 1, 8>(a, s, pass);
+            case 64: return v == 1 ? launch_vec<16, 1, 16>(a, s, pass) : launch_vec<16, 1, 8>(a, s, pass);
             case 128: return launch_vec<32, 1, 8>(a, s, pass);
             case 256: return launch_vec<64, 1, 8>(a, s, pass);
             case 512: return launch_vec<64, 2, 4>(a, s, pass);

@@ -117,6 +117,29 @@ def test_bit_exact_unsplit(gpu, name):
     assert np.array_equal(gi.cpu().numpy(), oi)
 
 
+@pytest.mark.parametrize("d", [4, 16, 64, 128, 256, 512, 1024])
+@pytest.mark.parametrize("variant", ["2", "3"])
+def test_tail_paths_bit_exact(gpu, monkeypatch, d, variant):
+    """Both item-pass tail paths (LGCN_SPMM_VARIANT 2 = predicated tail forced on, 3 = forced
+    off; the default picks per width and launch size) add in CSR order: unsplit rows of every
+    length 1..max are bitwise the oracle, forward and backward."""
+    from lgcn_amd import propagate_backward, propagate_forward
+
+    monkeypatch.setenv("LGCN_SPMM_VARIANT", variant)
+    U, I, ei = graphs.sym()
+    N, K = U + I, 2
+    plan = _plan(ei, N, gpu, chunk=1 << 20)
+    uw, iw = graphs.embeddings(U, I, d, seed=d)
+    out = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, K)
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
+    assert np.array_equal(out.cpu().numpy(), np.concatenate([ru, ri]))
+    dF = np.random.default_rng(d).standard_normal((N, d)).astype(np.float32)
+    gu, gi = propagate_backward(torch.from_numpy(dF).to(gpu), plan, U, K)
+    ou, oi = c_oracle.lightgcn_backward(dF, ei, U, K)
+    assert np.array_equal(gu.cpu().numpy(), ou)
+    assert np.array_equal(gi.cpu().numpy(), oi)
+
+
 @pytest.mark.parametrize("d", [3, 4, 8, 16, 32, 96, 128, 256, 512, 200])
 def test_widths(gpu, d):
     """Vector kernels (d in {4..1024} powers of two) and the scalar path (other d)."""
