@@ -211,6 +211,19 @@ int lgcn_spmm_run(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t*
                   float* acc_hi, int64_t acc_split, float* partial, int32_t mode, float div, float mul,
                   lgcn_stream_t stream, float* run);
 
+/* One launch instead of lgcn_spmm's two (item pass + combine), for schedules whose split rows
+ * have few chunks (Cluster-GCN batch plans): workgroup s < n_splits sums split row s itself —
+ * its pcnt chunk items chunks[pbeg .. pbeg+pcnt) (lgcn_item_t, in partial-slot order; items keep
+ * the row items only) — in the same association as item pass + combine (lane group g adds chunks
+ * g, g+G, ... then the G group sums in order), so the result is bitwise lgcn_spmm's; `partial`
+ * is unused (may be NULL). Vector widths only (d in {4, 8, ..., 1024}, 16-byte aligned rows).
+ * Replaces the same reference code as lgcn_spmm (models/light_gcn.py:33, LGConv.propagate). */
+int lgcn_spmm_blocksplit(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* splits, int64_t n_splits,
+                         const int32_t* col, const float* val, int64_t N, int32_t d, const float* x_lo,
+                         const float* x_hi, int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split,
+                         float* y, float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
+                         float div, float mul, lgcn_stream_t stream, const lgcn_item_t* chunks);
+
 /* out[i] = (in[i] * mul) / div over n floats: the gradient that MulBackward (× 1/(K+1))
  * then MeanBackward (÷ (K+1)) hand to every layer output (reference models/light_gcn.py:36). */
 int lgcn_scale(const float* in, float* out, int64_t n, float mul, float div, lgcn_stream_t stream);

@@ -52,6 +52,7 @@ struct SpmmArgs {
     float div;
     float mul;
     float* run;  // sliced launches: running row sums between a row's source-slice segments
+    const lgcn_item_t* chunks;  // block-split launches: split rows' chunk items, partial-slot order
 };
 
 // Sliced-schedule item flags, in the high bits of lgcn_item_t::len (rows, not partial chunks).
@@ -111,38 +112,15 @@ __device__ __forceinline__ void finish_row_vec(const SpmmArgs& a, int64_t r, int
     }
 }
 
-// The item pass. Group g of the block owns item blockIdx*GPB + g. Per 16-edge (LPR-edge) batch
-// the lanes load (col, val) coalesced — the NEXT batch's pair is loaded before the current
-// batch's gathers are issued, so that latency overlaps them — then UNROLL neighbour rows are
-// gathered (one float4 per lane each) before the first add, and added in CSR order.
-// SLICED: one launch of a source-sliced schedule (lgcn_spmm_run). A row item continues the row's
-// running sum from a.run unless it is the row's FIRST segment, and runs the epilogue only on its
-// LAST one; the sum stays one sequential chain in CSR order across launches.
-template <int LPR, int NV, int UNROLL, bool SLICED = false, int TAIL = 0>
-__global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
-    constexpr int GPB = kBlock / LPR;
-    const int g = threadIdx.x / LPR;
-    const int l = threadIdx.x % LPR;
-    const int64_t item = int64_t(blockIdx.x) * GPB + g;
-    if (item >= a.n_items) return;
-    lgcn_item_t it = a.items[item];
-    int32_t flags = kItemFirst | kItemLast;
-    if (SLICED && it.dst >= 0) {
-        flags = it.len & (kItemFirst | kItemLast);
-        it.len &= kItemLenMask;
-    }
+// Sum of one item's edges into acc, in CSR order. Per 16-edge (LPR-edge) batch the lanes load
+// (col, val) coalesced — the NEXT batch's pair is loaded before the current batch's gathers are
+// issued, so that latency overlaps them — then UNROLL neighbour rows are gathered (one float4 per
+// lane each) before the first add, and added in CSR order.
+template <int LPR, int NV, int UNROLL, int TAIL>
+__device__ __forceinline__ void sum_item(const SpmmArgs& a, const lgcn_item_t it, int l, float4 (&acc)[NV]) {
     const int64_t d4 = int64_t(LPR) * NV;
     const float4* __restrict__ xlo = reinterpret_cast<const float4*>(a.x_lo) + l;
     const float4* __restrict__ xhi = reinterpret_cast<const float4*>(a.x_hi) + l;
-    float4 acc[NV];
-    if (SLICED && !(flags & kItemFirst)) {
-        const float4* r = reinterpret_cast<const float4*>(a.run) + int64_t(it.dst) * d4 + l;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = r[k * LPR];
-    } else {
-#pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
     int cn = 0;
     float wn = 0.f;
     if (l < it.len) {
@@ -207,6 +185,73 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
             for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wj, src[k * LPR]);
         }
     }
+}
+
+// Block-split launches (lgcn_spmm_blocksplit): workgroup s < n_splits sums split row s whole.
+// Group g sums chunks g, g+GPB, ... (each from 0, in CSR order — the partial the item pass would
+// have written) into its running sum in that order, and the GPB sums are added in group order
+// through LDS: the association of item pass + k_combine_vec, so bitwise the same result,
+// without the partials' round trip or the second launch.
+template <int LPR, int NV, int UNROLL, int TAIL>
+__device__ __forceinline__ void split_row_block(const SpmmArgs& a, int64_t s, int g, int l) {
+    constexpr int GPB = kBlock / LPR;
+    __shared__ float4 lds[GPB][LPR * NV];
+    const lgcn_split_t sp = a.splits[s];
+    float4 acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int c = g; c < sp.pcnt; c += GPB) {
+        float4 part[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) part[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        sum_item<LPR, NV, UNROLL, TAIL>(a, a.chunks[int64_t(sp.pbeg) + c], l, part);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], part[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) lds[g][l + k * LPR] = acc[k];
+    __syncthreads();
+    if (g != 0) return;
+    const int ng = sp.pcnt < GPB ? sp.pcnt : GPB;
+    for (int h = 1; h < ng; ++h)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], lds[h][l + k * LPR]);
+    finish_row_vec<LPR, NV>(a, sp.row, l, acc);
+}
+
+// The item pass. Group g of the block owns item blockIdx*GPB + g (summed by sum_item).
+// SLICED: one launch of a source-sliced schedule (lgcn_spmm_run). A row item continues the row's
+// running sum from a.run unless it is the row's FIRST segment, and runs the epilogue only on its
+// LAST one; the sum stays one sequential chain in CSR order across launches.
+// BSPLIT: workgroups [0, n_splits) sum the split rows (split_row_block), the rest the items.
+template <int LPR, int NV, int UNROLL, bool SLICED = false, int TAIL = 0, bool BSPLIT = false>
+__global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
+    constexpr int GPB = kBlock / LPR;
+    const int g = threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    if (BSPLIT && int64_t(blockIdx.x) < a.n_splits) {
+        split_row_block<LPR, NV, UNROLL, TAIL>(a, blockIdx.x, g, l);
+        return;
+    }
+    const int64_t item = (int64_t(blockIdx.x) - (BSPLIT ? a.n_splits : 0)) * GPB + g;
+    if (item >= a.n_items) return;
+    lgcn_item_t it = a.items[item];
+    int32_t flags = kItemFirst | kItemLast;
+    if (SLICED && it.dst >= 0) {
+        flags = it.len & (kItemFirst | kItemLast);
+        it.len &= kItemLenMask;
+    }
+    const int64_t d4 = int64_t(LPR) * NV;
+    float4 acc[NV];
+    if (SLICED && !(flags & kItemFirst)) {
+        const float4* r = reinterpret_cast<const float4*>(a.run) + int64_t(it.dst) * d4 + l;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = r[k * LPR];
+    } else {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    sum_item<LPR, NV, UNROLL, TAIL>(a, it, l, acc);
     if (it.dst < 0) {
         float4* p = reinterpret_cast<float4*>(a.partial) + int64_t(-it.dst - 1) * d4 + l;
 #pragma unroll
@@ -338,11 +383,19 @@ __global__ __launch_bounds__(kBlock) void k_combine_scalar(SpmmArgs a) {
     finish_row_scalar(a, sp.row, l, acc);
 }
 
-enum { PASS_ITEMS = 1, PASS_COMBINE = 2, PASS_BOTH = 3 };
+enum { PASS_ITEMS = 1, PASS_COMBINE = 2, PASS_BOTH = 3, PASS_BSPLIT = 4 };
 
 template <int LPR, int NV, int UNROLL, int TAIL = 0>
 int launch_vec(const SpmmArgs& a, hipStream_t s, int pass) {
     constexpr int GPB = kBlock / LPR;
+    if (pass == PASS_BSPLIT) {  // split rows (one workgroup each) and items in one launch
+        const int64_t blocks = a.n_splits + (a.n_items + GPB - 1) / GPB;
+        if (blocks > 0) {
+            k_spmm_vec<LPR, NV, UNROLL, false, TAIL, true><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+            if (int rc = check_launch("k_spmm_vec")) return rc;
+        }
+        return LGCN_OK;
+    }
     if ((pass & PASS_ITEMS) && a.n_items > 0) {
         const int64_t blocks = (a.n_items + GPB - 1) / GPB;
         if (a.run != nullptr)
@@ -403,7 +456,8 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
               const int32_t* col, const float* val, int64_t N, int32_t d, const float* x_lo,
               const float* x_hi, int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split,
               float* y, float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
-              float div, float mul, lgcn_stream_t stream, int pass, float* run = nullptr) {
+              float div, float mul, lgcn_stream_t stream, int pass, float* run = nullptr,
+              const lgcn_item_t* chunks = nullptr) {
     if (N < 0 || d <= 0 || n_items < 0 || n_splits < 0)
         return fail(LGCN_E_ARG, "lgcn_spmm: bad sizes (N=%lld d=%d)", (long long)N, d);
     if (mode < LGCN_EPI_INIT || mode > LGCN_EPI_SCALE) return fail(LGCN_E_ARG, "lgcn_spmm: bad mode %d", mode);
@@ -415,12 +469,17 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
     const bool needs_e = (mode == LGCN_EPI_INIT || mode == LGCN_EPI_FINAL_E);
     if (needs_e && (!e_lo || (e_split < N && !e_hi)))
         return fail(LGCN_E_ARG, "lgcn_spmm: mode %d needs the e table", mode);
-    if (n_splits > 0 && (!splits || !partial)) return fail(LGCN_E_ARG, "lgcn_spmm: splits need partial scratch");
+    if (pass == PASS_BSPLIT) {
+        if (n_splits > 0 && (!splits || !chunks))
+            return fail(LGCN_E_ARG, "lgcn_spmm_blocksplit: splits need their chunk items");
+    } else if (n_splits > 0 && (!splits || !partial)) {
+        return fail(LGCN_E_ARG, "lgcn_spmm: splits need partial scratch");
+    }
     if (d > 64 * KMAX && d % 4 != 0)
         return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm: d=%d unsupported (d > %d needs d %% 4 == 0)", d, 64 * KMAX);
 
     SpmmArgs a{items, n_items, splits, n_splits, col, val, x_lo, x_hi, x_split, e_lo, e_hi, e_split,
-               y, acc_lo, acc_hi, acc_split, partial, d, mode, div, mul, run};
+               y, acc_lo, acc_hi, acc_split, partial, d, mode, div, mul, run, chunks};
     hipStream_t s = as_stream(stream);
 
     bool vec_ok = (d % 4 == 0) && aligned16(x_lo) && aligned16(acc_lo) && aligned16(partial) &&
@@ -464,6 +523,8 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
         }
     }
     if (run != nullptr) return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm_run: needs d in {4,8,...,1024} and aligned rows");
+    if (pass == PASS_BSPLIT)
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm_blocksplit: needs d in {4,8,...,1024} and aligned rows");
     if (d > 64 * KMAX) return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm: d=%d unsupported", d);
     return launch_scalar(a, s, pass);
 }
@@ -488,6 +549,9 @@ int lgcn_spmm_combine(LGCN_SPMM_PARAMS) { return spmm_impl(LGCN_SPMM_ARGS, PASS_
 int lgcn_spmm_run(LGCN_SPMM_PARAMS, float* run) {
     if (!run) return fail(LGCN_E_ARG, "lgcn_spmm_run: null running-sum buffer");
     return spmm_impl(LGCN_SPMM_ARGS, PASS_ITEMS, run);
+}
+int lgcn_spmm_blocksplit(LGCN_SPMM_PARAMS, const lgcn_item_t* chunks) {
+    return spmm_impl(LGCN_SPMM_ARGS, PASS_BSPLIT, nullptr, chunks);
 }
 
 int lgcn_scale(const float* in, float* out, int64_t n, float mul, float div, lgcn_stream_t stream) {

@@ -53,6 +53,9 @@ _SIGS = {
     "lgcn_spmm_run": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
                        _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp],
                       ctypes.c_int),
+    "lgcn_spmm_blocksplit": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
+                              _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp],
+                             ctypes.c_int),
     "lgcn_scale": ([_vp, _vp, _i64, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_copy_scale": ([_vp, _vp, _i64, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_bpr_fused": ([_vp, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _f32, _f32, _f32, _vp, _vp,

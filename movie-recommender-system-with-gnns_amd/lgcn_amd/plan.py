@@ -23,6 +23,9 @@ import torch
 from . import _ffi
 
 DEFAULT_CHUNK = 256
+# batch plans (touched-only, segment) use the one-launch block-split schedule; LGCN_BLOCKSPLIT=0
+# keeps them on item pass + combine (A/B knob)
+BLOCK_SPLIT = os.environ.get("LGCN_BLOCKSPLIT", "1") != "0"
 
 
 def slice_bytes_for(num_nodes: int, d: int) -> int:
@@ -54,6 +57,23 @@ class CsrDirection:
     n_splits: int
     n_partials: int
     chunk: int
+    # one-launch schedule (lgcn_spmm_blocksplit): split rows summed by one workgroup each, in the
+    # combine pass's association. For plans whose split rows have few chunks (batch plans).
+    block_split: bool = False
+
+    def block_lists(self):
+        """(row items [n, 2] int64, n, chunk items [n_partials, 2] in partial-slot order) for
+        lgcn_spmm_blocksplit; built on first use (one host sync) and cached."""
+        cached = getattr(self, "_block_lists", None)
+        if cached is None:
+            it = self.items[: self.n_items]
+            dst = it[:, 1].contiguous().view(torch.int32).view(-1, 2)[:, 1]
+            part = dst < 0
+            rows = it[~part].contiguous()
+            chunks = torch.empty((max(self.n_partials, 1), 2), dtype=torch.int64, device=it.device)
+            chunks[(-dst[part] - 1).long()] = it[part]
+            cached = self._block_lists = (rows, int(rows.shape[0]), chunks)
+        return cached
 
     def item_table(self) -> torch.Tensor:
         """Items as int64 [n_items, 3] = (beg, len, dst) — for tests."""
@@ -105,14 +125,15 @@ def segment_directions(keys: torch.Tensor, N: int, chunk: int = DEFAULT_CHUNK, r
     rowptr = rowptr_b[: N + 1].contiguous()
     val = torch.ones(M, dtype=torch.float32, device=dev)
     mask = (rowptr[1:] > rowptr[:-1]).to(torch.uint8)
-    dense = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, None, stream), chunk)
-    sparse = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, mask, stream), chunk)
+    dense = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, None, stream), chunk, BLOCK_SPLIT)
+    sparse = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, mask, stream), chunk, BLOCK_SPLIT)
     if int(err.item()):
         raise IndexError("segment keys out of range")
     if row_mask is None:
         return dense, sparse
     # every row of row_mask (0 where it has no contribution), e.g. a batch's touched rows
-    masked = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, row_mask, stream), chunk)
+    masked = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, row_mask, stream), chunk,
+                          BLOCK_SPLIT)
     return dense, sparse, masked
 
 
@@ -151,7 +172,9 @@ def _build_direction(key: torch.Tensor, other: torch.Tensor, N: int, chunk: int,
     host = torch.cat([counts, err]).cpu()
     n_items, n_splits, n_partials, n_bad = (int(v) for v in host.tolist())
     del ws, ws2
-    return CsrDirection(rowptr, col, eid, val, items, splits, n_items, n_splits, n_partials, chunk), dis, n_bad
+    # touched-only (Cluster-GCN batch) plans: short chunks, few per split row -> one launch per layer
+    return CsrDirection(rowptr, col, eid, val, items, splits, n_items, n_splits, n_partials, chunk,
+                        BLOCK_SPLIT and row_mask is not None), dis, n_bad
 
 
 class PropagationPlan:

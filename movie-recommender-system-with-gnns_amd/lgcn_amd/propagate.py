@@ -57,6 +57,20 @@ def spmm(direction, N: int, d: int, x, e, acc, y, mode: int, div: float = 1.0, m
     xl, xh, xs = x
     el, eh, es = e if e is not None else (None, None, N)
     al, ah, as_ = acc
+    if direction.block_split and direction.n_splits and d % 4 == 0 and d <= 1024 and (d & (d - 1)) == 0:
+        # one launch: split rows summed by one workgroup each (bitwise the items + combine pair)
+        rows, n_rows, chunks = direction.block_lists()
+        args = (rows.data_ptr(), n_rows, direction.splits.data_ptr(), direction.n_splits,
+                direction.col.data_ptr(), direction.val.data_ptr(), N, d,
+                _ffi.ptr(xl), _ffi.ptr(xh), xs, _ffi.ptr(el), _ffi.ptr(eh), es,
+                _ffi.ptr(y), _ffi.ptr(al), _ffi.ptr(ah), as_, None, mode, div, mul, stream, chunks.data_ptr())
+        if _launch_timer is not None:
+            with _launch_timer(d):
+                rc = lib.lgcn_spmm_blocksplit(*args)
+        else:
+            rc = lib.lgcn_spmm_blocksplit(*args)
+        _ffi.check(rc, "lgcn_spmm_blocksplit")
+        return
     args = (direction.items.data_ptr(), direction.n_items, direction.splits.data_ptr(), direction.n_splits,
             direction.col.data_ptr(), direction.val.data_ptr(), N, d,
             _ffi.ptr(xl), _ffi.ptr(xh), xs, _ffi.ptr(el), _ffi.ptr(eh), es,

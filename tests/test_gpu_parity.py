@@ -140,6 +140,53 @@ def test_tail_paths_bit_exact(gpu, monkeypatch, d, variant):
     assert np.array_equal(gi.cpu().numpy(), oi)
 
 
+@pytest.mark.parametrize("d", [4, 16, 64, 128, 256, 512, 1024])
+@pytest.mark.parametrize("chunk", [3, 32])
+def test_blocksplit_equals_items_plus_combine(gpu, d, chunk):
+    """lgcn_spmm_blocksplit (split rows summed by one workgroup each, one launch) is bitwise the
+    item pass + combine pair, forward and backward, with split rows of 2..700 chunks; and both
+    are within 1e-5 of the oracle."""
+    from lgcn_amd import propagate_backward, propagate_forward
+
+    U, I, ei = graphs.hub()
+    N, K = U + I, 2
+    plan = _plan(ei, N, gpu, chunk=chunk)
+    assert plan.fwd.n_splits > 0 and plan.bwd.n_splits > 0
+    uw, iw = graphs.embeddings(U, I, d, seed=d)
+    dF = np.random.default_rng(d).standard_normal((N, d)).astype(np.float32)
+    res = []
+    for bs in (False, True):
+        plan.fwd.block_split = plan.bwd.block_split = bs
+        out = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, K)
+        gu, gi = propagate_backward(torch.from_numpy(dF).to(gpu), plan, U, K)
+        res.append((out.cpu(), gu.cpu(), gi.cpu()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
+    assert rel_err(res[1][0].numpy(), np.concatenate([ru, ri])) <= RTOL
+
+
+def test_blocksplit_argument_errors(gpu):
+    """The one-launch entry point refuses split rows without their chunk list, and widths the
+    vector kernels do not cover (no silent fallback)."""
+    from lgcn_amd import _ffi
+
+    U, I, ei = graphs.hub()
+    N = U + I
+    plan = _plan(ei, N, gpu, chunk=8)
+    f = plan.fwd
+    rows, n_rows, chunks = f.block_lists()
+    lib = _ffi.load()
+    s = _ffi.stream_of(gpu)
+    common = (rows.data_ptr(), n_rows, f.splits.data_ptr(), f.n_splits, f.col.data_ptr(), f.val.data_ptr(), N)
+    for d, ch, code in ((16, None, -1), (12, chunks.data_ptr(), -3)):
+        x = torch.zeros((N, d), device=gpu)
+        y = torch.zeros((N, d), device=gpu)
+        rc = lib.lgcn_spmm_blocksplit(*common, d, x.data_ptr(), None, N, None, None, N, None, y.data_ptr(), None, N,
+                                      None, _ffi.EPI_STORE, 1.0, 1.0, s, ch)
+        assert rc == code, lib.lgcn_last_error()
+
+
 @pytest.mark.parametrize("d", [3, 4, 8, 16, 32, 96, 128, 256, 512, 200])
 def test_widths(gpu, d):
     """Vector kernels (d in {4..1024} powers of two) and the scalar path (other d)."""
