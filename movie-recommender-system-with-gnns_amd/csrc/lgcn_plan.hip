@@ -173,49 +173,65 @@ __device__ __forceinline__ int slice_of(int64_t c, const int64_t* __restrict__ b
     return lo;
 }
 
-// One thread per row: its segments (runs of one source slice), hub flag (a segment longer than
-// chunk), item / partial counts, and whether its neighbours are ascending.
+// A row's slice segments: [start, end) runs of its CSR list whose neighbours fall in one source
+// slice, visited in ascending slice order. Found by binary search of the slice bounds in the row's
+// (ascending) neighbour list — O(segments * log deg) per row instead of a scan of every edge. On an
+// unsorted row (flagged by k_slice_count; the host then discards the schedule) the searches still
+// return positions inside [start, end), so every segment stays in bounds and count / fill agree.
+template <class F>
+__device__ __forceinline__ void for_each_segment(const int32_t* __restrict__ col, int64_t beg, int64_t end,
+                                                 const int64_t* __restrict__ bounds, int S, F&& f) {
+    int sl = slice_of(col[beg], bounds, S);
+    int64_t start = beg;
+    while (start < end) {
+        int64_t stop = end;
+        if (sl < S - 1) {  // lower bound of bounds[sl + 1] in col[start, end)
+            const int64_t b = bounds[sl + 1];
+            int64_t lo = start, hi = end;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (col[mid] < b) lo = mid + 1;
+                else hi = mid;
+            }
+            stop = lo;
+        }
+        if (stop > start) f(start, stop, sl);
+        start = stop;
+        ++sl;
+    }
+}
+
+// One wave per row: the lanes check that its neighbours ascend (coalesced), lane 0 counts its
+// segments, chunks (hub: a segment longer than chunk) and items.
 __global__ void k_slice_count(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col, int64_t N,
                               const int64_t* __restrict__ bounds, int S, int32_t chunk,
                               int64_t* __restrict__ n_items, int32_t* __restrict__ n_part,
                               int32_t* __restrict__ n_split, int32_t* __restrict__ unsorted) {
-    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += stride) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+    for (int64_t i = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; i < N; i += nwaves) {
         const int64_t beg = rowptr[i], end = rowptr[i + 1];
+        bool bad = false;
+        for (int64_t e = beg + 1 + lane; e < end; e += 64) bad |= col[e] < col[e - 1];
+        if (__any(bad) && lane == 0) atomicOr(unsorted, 1);
+        if (lane != 0) continue;
         if (end == beg) {
             n_items[i] = 1;
             n_part[i] = 0;
             n_split[i] = 0;
             continue;
         }
-        int64_t segs = 0, chunks = 0, maxlen = 0, len = 0;
-        int cur = -1;
-        int32_t prev = -1;
-        bool bad = false;
-        for (int64_t e = beg; e < end; ++e) {
-            const int32_t c = col[e];
-            bad |= c < prev;
-            prev = c;
-            const int sl = slice_of(c, bounds, S);
-            if (sl != cur) {
-                if (len) {
-                    ++segs;
-                    chunks += (len + chunk - 1) / chunk;
-                    maxlen = len > maxlen ? len : maxlen;
-                }
-                cur = sl;
-                len = 0;
-            }
-            ++len;
-        }
-        ++segs;
-        chunks += (len + chunk - 1) / chunk;
-        maxlen = len > maxlen ? len : maxlen;
+        int64_t segs = 0, chunks = 0, maxlen = 0;
+        for_each_segment(col, beg, end, bounds, S, [&](int64_t a, int64_t b, int) {
+            const int64_t len = b - a;
+            ++segs;
+            chunks += (len + chunk - 1) / chunk;
+            maxlen = len > maxlen ? len : maxlen;
+        });
         const bool hub = maxlen > chunk;
         n_items[i] = hub ? chunks : segs;
         n_part[i] = hub ? static_cast<int32_t>(chunks) : 0;
         n_split[i] = hub ? 1 : 0;
-        if (bad) atomicOr(unsorted, 1);
     }
 }
 
@@ -247,25 +263,19 @@ __global__ void k_slice_fill(const int64_t* __restrict__ rowptr, const int32_t* 
         } else {
             const bool hub = n_part[i] > 0;
             int32_t pk = 0;  // hub rows: next partial slot, in CSR order
-            int64_t sb = beg;
-            int cur = slice_of(col[beg], bounds, S);
-            for (int64_t e = beg + 1; e <= end; ++e) {
-                const int sl = (e < end) ? slice_of(col[e], bounds, S) : -1;
-                if (sl == cur) continue;
-                const int64_t len = e - sb;  // segment [sb, e) in slice cur
+            for_each_segment(col, beg, end, bounds, S, [&](int64_t sb, int64_t e, int sl) {
+                const int64_t len = e - sb;
                 if (hub) {
                     for (int64_t c0 = 0; c0 < len; c0 += chunk) {
                         const int32_t l = static_cast<int32_t>(len - c0 < chunk ? len - c0 : chunk);
-                        emit(sb + c0, l, -(part_off[i] + pk) - 1, cur, l);
+                        emit(sb + c0, l, -(part_off[i] + pk) - 1, sl, l);
                         ++pk;
                     }
                 } else {
                     const int32_t flags = (sb == beg ? kSliceFirst : 0) | (e == end ? kSliceLast : 0);
-                    emit(sb, static_cast<int32_t>(len) | flags, static_cast<int32_t>(i), cur, static_cast<int32_t>(len));
+                    emit(sb, static_cast<int32_t>(len) | flags, static_cast<int32_t>(i), sl, static_cast<int32_t>(len));
                 }
-                sb = e;
-                cur = sl;
-            }
+            });
             if (hub) {
                 lgcn_split_t sp;
                 sp.row = static_cast<int32_t>(i);
@@ -598,7 +608,8 @@ int lgcn_slice_schedule_build(const int64_t* rowptr, const int32_t* col, int64_t
     // counts[3] = 1 if some row's neighbours are not ascending (the caller falls back)
     if (int rc = check_hip(hipMemsetAsync(counts, 0, 4 * sizeof(int64_t), s), "memset counts")) return rc;
     const unsigned g = grid_for(N, kBlock, 8192);
-    k_slice_count<<<g, kBlock, 0, s>>>(rowptr, col, N, bounds, S, chunk, n_items, n_part, n_split,
+    k_slice_count<<<grid_for(N * 64, kBlock, 8192), kBlock, 0, s>>>(rowptr, col, N, bounds, S, chunk, n_items, n_part,
+                                                                     n_split,
                                        reinterpret_cast<int32_t*>(counts + 3));
     if (int rc = check_launch("k_slice_count")) return rc;
     size_t t = cub_bytes;
