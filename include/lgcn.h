@@ -265,7 +265,8 @@ int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C
  * in b order, of C[b]) * mul / div for keys in [0, nrows). Workgroup w owns a key range and keeps
  * its keys in b order by an ordered block compaction; used for the per-step negatives.
  * Optional second source C2 (nullable): the same per-row sums of C2 are parked in c2buf[b_first]
- * (c2flag[b_first] = 1; the launch clears c2flag) for lgcn_flagged_rows_add to add LATER (the
+ * (the launch writes c2flag[b] for every b: 1 on a row's first occurrence, else 0 — no memset
+ * needed) for lgcn_flagged_rows_add to add LATER (the
  * negatives' reg-gradient rows must land after the backward). *overflow (nullable, caller-zeroed)
  * is set if a workgroup's list overflowed — parked sums would then be split; callers check it.
  * store_unless (nullable, uint8[rows]): a row with store_unless[row] == 0 is STORED (not added

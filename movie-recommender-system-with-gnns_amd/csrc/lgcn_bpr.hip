@@ -268,6 +268,8 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
             for (int j = 0; j < kRSChunks; ++j) {
                 const int64_t bj = base + (int64_t(wv) * kRSChunks + j) * 64 + lane;
                 kv[j] = bj < B ? keys[bj] : -1;
+                // keys no workgroup owns (outside [0, nrows)): workgroup 0 clears their flag
+                if (C2 && blockIdx.x == 0 && bj < B && (kv[j] < 0 || kv[j] >= nrows)) c2flag[bj] = 0;
             }
 #pragma unroll
             for (int j = 0; j < kRSChunks; ++j) {
@@ -311,6 +313,8 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                     first = false;
                     break;
                 }
+            // every b is in exactly one list: its flag is written here (1 = the row's parked C2 sum)
+            if (C2 && l == 0) c2flag[lidx[e]] = first ? 1 : 0;
             if (!first) continue;
             float4 acc[NV], acc2[NV];
 #pragma unroll
@@ -339,7 +343,6 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                 float4* cb = reinterpret_cast<float4*>(c2buf + int64_t(lidx[e]) * d) + l;
 #pragma unroll
                 for (int k = 0; k < NV; ++k) cb[k * LPR] = acc2[k];
-                if (l == 0) c2flag[lidx[e]] = 1;
             }
             const int64_t row = lo + key + key_offset;
             float4* o = reinterpret_cast<float4*>(srow(out_lo, out_hi, split, row, int64_t(d))) + l;
@@ -397,9 +400,6 @@ int launch_rs(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset,
     if (wgs > nrows) wgs = nrows > 0 ? nrows : 1;
     const int64_t span = (nrows + wgs - 1) / wgs;
     const int64_t grid = (nrows + span - 1) / span;
-    if (C2) {
-        if (int rc = check_hip(hipMemsetAsync(c2flag, 0, static_cast<size_t>(B), s), "memset c2flag")) return rc;
-    }
     k_range_scatter<LPR, NV><<<dim3(static_cast<unsigned>(grid)), kRSBlock, 0, s>>>(keys, B, nrows, span, key_offset, C, d,
                                                                                  lo, hi, split, mul, div, C2, c2buf,
                                                                                  c2flag, overflow, store_unless);
@@ -471,7 +471,10 @@ int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_
                            const uint8_t* store_unless, lgcn_stream_t stream) {
     if (B < 0 || d <= 0 || nrows < 0 || (B > 0 && (!keys || !C || !out_lo)) || (C2 && (!c2buf || !c2flag)))
         return fail(LGCN_E_ARG, "lgcn_range_scatter_add: bad args");
-    if (B == 0 || nrows == 0) return LGCN_OK;
+    if (B == 0) return LGCN_OK;
+    if (nrows == 0)  // no key is in range: nothing to add, every flag 0
+        return C2 ? check_hip(hipMemsetAsync(c2flag, 0, static_cast<size_t>(B), as_stream(stream)), "memset c2flag")
+                  : LGCN_OK;
     if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C2 && (!al16(C2) || !al16(c2buf))))
         return fail(LGCN_E_UNSUPPORTED, "lgcn_range_scatter_add: needs d %% 4 == 0 and aligned rows");
     hipStream_t s = as_stream(stream);
