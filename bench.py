@@ -4,21 +4,25 @@ Workload (BASELINE.json configs[1]): MovieLens-25M-shaped ful
 (U=162,541, I=59,047, 12.45M unique rating>=4 pairs -> E = 24.9M directed edges), K=3, d=64,
 fp32. One step = one full K-layer forward propagation (LightGCN.forward semantics, reference
 models/light_gcn.py:28-40) with the plan (CSR + gcn_norm + schedule) already built and the
-embedding tables resident in HBM. value = K * E * (graphs processed) / wall time.
+embedding tables resident in HBM. value = K * E / wall time per step: ONE graph at every N.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
-GPU. C2 is replicas only (the full-graph SpMM does not split without a per-layer
-exchange): each rank propagates its own independent graph instance (seed = rank), no data-path
-collective (scaling: weak). C5 (--config c5) is feature-sharded: one graph, d/N columns per
-rank, no collective (scaling: strong). The barrier and the max-over-ranks time go over RCCL.
+GPU, strong scaling. C2 is row-sharded (lgcn_amd.sharded): each rank propagates its own
+edge-balanced destination rows of the same graph, and each layer's two output blocks (user rows,
+item rows) are all-gathered over RCCL on a side stream while the other half-layer computes;
+the result is bitwise the 1-GPU result. C5 (--config c5) is feature-sharded: d/N columns per
+rank, no collective. The barrier and the max-over-ranks time go over RCCL.
 
 Also reported (one JSON line on rank 0):
-  roofline     — achieved algorithmic GB/s of the dominant kernel (the item pass, k_spmm_vec;
-                 at C2 one launch per source slice, lgcn_amd.sliced), timed live with HIP events
-                 on its launching stream, vs the 8 TB/s HBM peak; bytes per layer =
-                 E*(4d+8) + N*(4d+8), per launch = that / launches per layer.
+  roofline     — the dominant kernel (the item pass, k_spmm_vec; at C2 one launch per source
+                 slice, lgcn_amd.sliced), its launch time measured live with HIP events on its
+                 launching stream. achieved = memory-side bytes per launch (rocprofv3 FETCH_SIZE
+                 x calibration + WRITE_SIZE, profiles/pmc_traffic.json, measured on this workload)
+                 / launch time, frac = achieved / 8 TB/s; without a PMC entry the compulsory bytes
+                 of the schedule stand in (basis "compulsory", a lower bound). Also: the schedule's
+                 compulsory bytes, SURVEY §8d's no-reuse algorithmic bytes as effective_GBps.
   cpu_baseline — the reference's CPU op sequence (PyG 2.4.0 LGConv restated with torch CPU
-                 primitives, oracle/lgconv_torch.py) on a bounded sample, rank 0, N=1 only.
+                 primitives, oracle/lgconv_torch.py) on the whole C2 graph, rank 0, N=1 only.
 """
 from __future__ import annotations
 
@@ -41,7 +45,8 @@ def log(*a):
 
 
 class LaunchTimer:
-    """HIP-event brackets around each dominant-kernel launch, on the launching stream."""
+    """HIP-event brackets around the dominant kernel's launches, on the launching stream; each
+    bracket covers n item-pass launches (a layer's source slices)."""
 
     def __init__(self):
         import torch
@@ -50,7 +55,7 @@ class LaunchTimer:
         self.pairs = []
         self.active = False
 
-    def __call__(self, d):
+    def __call__(self, d, n=1):
         timer = self
 
         class _Ctx:
@@ -64,15 +69,16 @@ class LaunchTimer:
                 if timer.active:
                     e = timer.torch.cuda.Event(enable_timing=True)
                     e.record(timer.torch.cuda.current_stream())
-                    timer.pairs.append((self_.s, e))
+                    timer.pairs.append((self_.s, e, n))
                 return False
 
         return _Ctx()
 
     def mean_ms(self):
+        """Average time of one launch (brackets include the ~1.5 us gaps between a layer's slices)."""
         if not self.pairs:
             return None
-        return sum(s.elapsed_time(e) for s, e in self.pairs) / len(self.pairs)
+        return sum(s.elapsed_time(e) for s, e, _ in self.pairs) / sum(n for _, _, n in self.pairs)
 
 
 def load_traffic(workload: str):
@@ -103,35 +109,58 @@ def init_dist(backend, dev):
         dist.init_process_group(backend)
 
 
+def cpu_share():
+    """(CPUs in this process's affinity mask, cgroup CPU quota or None, physical cores of the machine)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    phys = None
+    try:
+        import psutil
+
+        phys = psutil.cpu_count(logical=False)
+    except Exception:
+        pass
+    return aff, quota, phys
+
+
 def cpu_baseline(graph, K, d, seconds_budget=20.0):
-    """Reference CPU path (torch primitives of PyG 2.4.0 LGConv) on a bounded edge sample."""
-    import numpy as np
+    """Reference CPU path (torch primitives of PyG 2.4.0 LGConv, oracle/lgconv_torch.py) on the
+    WHOLE C2 edge set, with every CPU of the affinity mask; when a cgroup quota
+    caps the process below that, the quota's thread count is timed too and the faster is kept."""
     import torch
 
     from oracle.lgconv_torch import time_csr_forward, time_reference_forward
 
-    threads = min(16, len(os.sched_getaffinity(0)))
-    torch.set_num_threads(threads)
-    E = graph.num_edges
-    frac = 0.1 if E > 5_000_000 else 1.0
-    rng = np.random.default_rng(0)
-    keep = np.sort(rng.choice(E, int(E * frac), replace=False)) if frac < 1 else np.arange(E)
-    ei = torch.from_numpy(np.ascontiguousarray(graph.edge_index[:, keep]))
+    aff, quota, phys = cpu_share()
+    counts = [aff] + ([quota] if quota and quota < aff else [])
+    ei = torch.from_numpy(graph.edge_index)
     g = torch.Generator().manual_seed(0)
     uw = torch.randn(graph.num_users, d, generator=g) * 0.01
     iw = torch.randn(graph.num_items, d, generator=g) * 0.01
-    t0 = time.perf_counter()
-    t = time_reference_forward(uw, iw, ei, K, reps=1)
-    reps = max(1, min(5, int(seconds_budget / max(t, 1e-3)) - 1))
-    if reps > 1:
-        t = time_reference_forward(uw, iw, ei, K, reps=reps)
-    log(f"cpu_baseline: {ei.shape[1]} edges, {threads} threads, {t:.3f} s/forward "
-        f"({time.perf_counter() - t0:.1f} s total)")
-    # second CPU baseline: the whole C2 graph as one CSR matrix, torch.sparse.mm per layer
-    full = torch.from_numpy(graph.edge_index)
+    runs = {}
+    for threads in counts:
+        torch.set_num_threads(threads)
+        t0 = time.perf_counter()
+        t = time_reference_forward(uw, iw, ei, K, reps=1, warmup=False)
+        reps = max(1, min(3, int(seconds_budget / max(t, 1e-3)) - 1))
+        if reps > 1:  # short enough: warm run + median of reps
+            t = time_reference_forward(uw, iw, ei, K, reps=reps)
+        runs[threads] = (t, reps)
+        log(f"cpu_baseline: all {ei.shape[1]} edges, {threads} threads, {t:.3f} s/forward "
+            f"({time.perf_counter() - t0:.1f} s total)")
+    threads = min(runs, key=lambda k: runs[k][0])
+    t, reps = runs[threads]
+    torch.set_num_threads(threads)
     t1 = time.perf_counter()
-    tc = time_csr_forward(uw, iw, full, K, reps=3)
-    log(f"cpu_baseline csr: {full.shape[1]} edges, {tc:.3f} s/forward ({time.perf_counter() - t1:.1f} s total)")
+    tc = time_csr_forward(uw, iw, ei, K, reps=3)
+    log(f"cpu_baseline csr: {ei.shape[1]} edges, {threads} threads, {tc:.3f} s/forward "
+        f"({time.perf_counter() - t1:.1f} s total)")
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -139,12 +168,43 @@ def cpu_baseline(graph, K, d, seconds_budget=20.0):
     except (OSError, StopIteration):
         pass
     return {"value": K * ei.shape[1] / t, "unit": "edges/s", "cores": threads, "kind": "port", "cpu_model": model,
-            "csr_spmm": {"value": K * full.shape[1] / tc, "unit": "edges/s", "cores": threads,
-                         "sample": f"all {full.shape[1]} C2 edges, K={K} d={d}: gcn_norm-weighted CSR built once, "
+            "affinity_cpus": aff, "cgroup_cpu_quota": quota, "physical_cores_machine": phys,
+            "threads_timed": {str(k): K * ei.shape[1] / v[0] for k, v in runs.items()},
+            "csr_spmm": {"value": K * ei.shape[1] / tc, "unit": "edges/s", "cores": threads,
+                         "sample": f"all {ei.shape[1]} C2 edges, K={K} d={d}: gcn_norm-weighted CSR built once, "
                                    f"torch.sparse.mm per layer + layer mean, median of 3"},
-            "sample": f"random {frac:.0%} of the C2 edges ({ei.shape[1]} edges, all {graph.num_nodes} nodes), "
-                      f"K={K} d={d} forward: index_select -> mul -> scatter_add_ with gcn_norm per layer "
-                      f"(PyG 2.4.0 LGConv op sequence, torch {torch.__version__} CPU), median of {reps}"}
+            "sample": f"all {ei.shape[1]} C2 edges (no sampling), all {graph.num_nodes} nodes, K={K} d={d} forward: "
+                      f"index_select -> mul -> scatter_add_ with gcn_norm per layer (PyG 2.4.0 LGConv op sequence, "
+                      f"torch {torch.__version__} CPU), median of {reps}"}
+
+
+def schedule_traffic(sched, n_src_rows: int, d: int):
+    """(compulsory bytes of one middle layer's item pass over `sched`, its launches, edges, rows
+    finished in the pass): every source
+    row read once, each edge's int32 index + fp32 weight, each lgcn_item_t, the ADD epilogue of
+    each row finished in the pass (y write + acc read + write), the running-sum read/write of each
+    non-FIRST / non-LAST slice segment, and the hub rows' partial slots written."""
+    import torch
+
+    from lgcn_amd.sliced import ITEM_FIRST, ITEM_LAST, SlicedDirection
+
+    row = 4 * d
+    if isinstance(sched, SlicedDirection):
+        n = sum(n for _, n in sched.launches)
+        ld = sched.items[:n, 1].contiguous().view(torch.int32).view(-1, 2)
+        ln, rowi = ld[:, 0], ld[:, 1] >= 0
+        run_rw = int(((ln & ITEM_FIRST) == 0)[rowi].sum()) + int(((ln & ITEM_LAST) == 0)[rowi].sum())
+        finished = int(((ln & ITEM_LAST) != 0)[rowi].sum())
+        edges = int((ln & 0x1FFFFFFF).sum())
+        launches = sched.n_launches
+    else:
+        n = sched.n_items
+        ld = sched.items[:n, 1].contiguous().view(torch.int32).view(-1, 2)
+        run_rw, finished, launches = 0, int((ld[:, 1] >= 0).sum()), 1
+        edges = int(ld[:, 0].sum())
+    per_layer = (n_src_rows * row + edges * 8 + n * 16 + finished * 3 * row + run_rw * row
+                 + sched.n_partials * row)
+    return per_layer, launches, edges, finished + sched.n_splits
 
 
 def main():
@@ -184,6 +244,7 @@ def main():
     import lgcn_amd
     from lgcn_amd import synth
     from lgcn_amd.plan import DEFAULT_CHUNK, PropagationPlan
+    from lgcn_amd.sliced import SlicedDirection
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -200,8 +261,10 @@ def main():
     K = args.layers if args.layers is not None else (4 if c5 else 3)
     d = args.dim if args.dim is not None else (256 if c5 else 64)
     d_full = d
+    chunk = args.chunk or DEFAULT_CHUNK
     t0 = time.perf_counter()
     graph = None
+    sharded = not c5 and distributed
     if c5:
         # C5: one synthetic 10M x 1M x 5e8-edge graph (same seed on every rank, generated on the GPU).
         # N > 1 ranks shard the embedding COLUMNS (feature-sharded propagation): every
@@ -216,36 +279,57 @@ def main():
         log(f"[rank {rank}] c5 graph U={U} I={I} E={E} on device, d={d_full} -> {d} columns per rank "
             f"({time.perf_counter() - t0:.1f} s)")
     else:
-        graph = synth.ml25m_shaped(seed=rank, scale=args.scale)
+        # C2: ONE graph (seed 0 on every rank); N > 1 ranks split its destination rows
+        graph = synth.ml25m_shaped(seed=0, scale=args.scale)
         log(f"[rank {rank}] graph U={graph.num_users} I={graph.num_items} E={graph.num_edges} "
             f"{graph.degree_stats()} ({time.perf_counter() - t0:.1f} s)")
         U, I, N, E = graph.num_users, graph.num_items, graph.num_nodes, graph.num_edges
         ei = torch.from_numpy(graph.edge_index).to(dev)
-    gen = torch.Generator(device=dev).manual_seed(rank)
+    # the model's tables: the same on every rank (seed 0)
+    gen = torch.Generator(device=dev).manual_seed(0)
     user_w = (torch.randn(U, d, device=dev, generator=gen) * 0.01).contiguous()
     item_w = (torch.randn(I, d, device=dev, generator=gen) * 0.01).contiguous()
     t0 = time.perf_counter()
-    # side_split = U: rows gathering the item table run first, then rows gathering the user table
-    plan = PropagationPlan(ei, N, args.chunk or DEFAULT_CHUNK, side_split=U)
-    # the schedule the forward runs at this width: source-sliced (one lgcn_spmm_run launch per
-    # slice per layer) when lgcn_amd.plan.slice_bytes_for enables it, else the plain item list
-    from lgcn_amd.sliced import SlicedDirection
+    exchange = None
+    if sharded:
+        from lgcn_amd.sharded import BlockExchange, RowShards, ShardedPlan, propagate_forward_sharded
 
-    sched = plan.schedule("fwd", d)
-    n_slices = sum(1 for _, n in sched.launches if n) if isinstance(sched, SlicedDirection) else 1
-    torch.cuda.synchronize()
-    log(f"[rank {rank}] plan: {plan.fwd.n_items} items, {plan.fwd.n_splits} split rows, "
-        f"{plan.fwd.n_partials} partials, {plan.nbytes() / 1e6:.0f} MB; "
-        f"{n_slices} source slice(s) per layer, {sched.n_splits} chunked rows ({time.perf_counter() - t0:.2f} s)")
+        shards = RowShards.build(np.bincount(graph.edge_index[1], minlength=N), U, world)
+        splan = ShardedPlan(ei, shards, rank, d, chunk)
+        x0p = shards.to_padded(user_w, item_w)
+        exchange = BlockExchange(shards, rank)
+        scheds = [h.direction for h in splan.halves]
+        torch.cuda.synchronize()
+        ua, ub_ = shards.user_rows(rank)
+        ia, ib_ = shards.item_rows(rank)
+        log(f"[rank {rank}] row shard: users {ub_ - ua} (of {U}), items {ib_ - ia} (of {I}), padded N {shards.NP}; "
+            f"{'sliced' if splan.sliced else 'plain'} halves, {time.perf_counter() - t0:.2f} s")
 
-    def step():
-        return lgcn_amd.propagate_forward(user_w, item_w, plan, K)
+        def step():
+            return propagate_forward_sharded(x0p, splan, K, exchange)
+    else:
+        # side_split = U: rows gathering the item table run first, then rows gathering the user table
+        plan = PropagationPlan(ei, N, chunk, side_split=U)
+        # the schedule the forward runs at this width: source-sliced (one item-pass launch per slice
+        # per layer) when lgcn_amd.plan.slice_bytes_for enables it, else the plain item list
+        sched = plan.schedule("fwd", d)
+        scheds = [sched]
+        torch.cuda.synchronize()
+        n_sl = sched.n_launches if isinstance(sched, SlicedDirection) else 1
+        log(f"[rank {rank}] plan: {plan.fwd.n_items} items, {plan.fwd.n_splits} split rows, "
+            f"{plan.fwd.n_partials} partials, {plan.nbytes() / 1e6:.0f} MB; "
+            f"{n_sl} source slice(s) per layer, {sched.n_splits} chunked rows ({time.perf_counter() - t0:.2f} s)")
+
+        def step():
+            return lgcn_amd.propagate_forward(user_w, item_w, plan, K)
 
     with torch.no_grad():
         for _ in range(args.warmup):
             step()
         timer = LaunchTimer()
         lgcn_amd.set_launch_timer(timer)
+        if exchange is not None:
+            exchange.bytes = 0
         if distributed:
             dist.barrier()
         torch.cuda.synchronize()
@@ -260,32 +344,36 @@ def main():
         timer.active = False
         lgcn_amd.set_launch_timer(None)
 
-    # the timer brackets each layer's item pass: n_slices launches (+ the short gaps between them)
-    kernel_ms = timer.mean_ms() / n_slices
-    edges_total = E
+    kernel_ms = timer.mean_ms()  # one item-pass launch, averaged over the timed region
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        e = torch.tensor([E], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.SUM)
-        edges_total = int(e.item())
-        km = torch.tensor([kernel_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        kernel_ms = float(km.item())
+        elapsed, kernel_ms = float(t[0].item()), float(t[1].item())
 
-    if c5:
-        edges_total = E  # feature-sharded: the ranks together propagate one graph
-    value = K * edges_total * args.steps / elapsed
-    # algorithmic bytes of one layer, spread over the layer's n_slices launches
-    bytes_per_layer = E * (4 * d + 8) + N * (4 * d + 8)
-    bytes_per_launch = bytes_per_layer / n_slices
-    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    # one graph in every configuration: C2 row-sharded / C5 column-sharded over the ranks
+    value = K * E * args.steps / elapsed
+    # bytes of one middle layer's item pass (this rank's rows), spread over its launches
+    comp_layer, launches, e_mine, n_mine = 0, 0, 0, 0
+    for sc in scheds:
+        b, n, e_s, r_s = schedule_traffic(sc, N, d)
+        comp_layer, launches, e_mine, n_mine = comp_layer + b, launches + n, e_mine + e_s, n_mine + r_s
+    comp_launch = comp_layer / launches
+    # SURVEY §8d's no-reuse algorithmic bytes (every gathered row counted per edge) of this rank's rows
+    alg_launch = (e_mine * (4 * d + 8) + n_mine * (4 * d + 8)) / launches
     if c5:
         workload = f"C5_synthetic_10Mx1M_5e8_K{K}_d{d_full}" + ("" if args.scale == 1.0 else f"_scale{args.scale}")
     else:
         workload = f"C2_ml25m_shaped_K{K}_d{d}" + ("" if args.scale == 1.0 else f"_scale{args.scale}")
-    traffic = load_traffic(workload)
+        if sharded:
+            workload += f"_rowshard{world}"
+    if c5 and world > 1:
+        workload_pmc = None
+    else:
+        workload_pmc = workload
+    traffic = load_traffic(workload_pmc) if workload_pmc else None
+    basis = "pmc_memory_side" if traffic else "compulsory"
+    achieved = (traffic if traffic else comp_launch) / (kernel_ms * 1e-3) / 1e9
+    sliced = isinstance(scheds[0], SlicedDirection)
     result = {
         "metric": f"edges propagated/sec (K={K}, d={d_full})",
         "value": value,
@@ -295,25 +383,34 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if c5 else "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "fp32",
         "data": ("synthetic (seeded 10M x 1M Zipf bipartite graph generated on device; random N(0,0.01) embeddings)"
-                 if c5 else "synthetic (seeded ML-25M-shaped bipartite graph per rank; random N(0,0.01) embeddings)"),
+                 if c5 else "synthetic (seeded ML-25M-shaped bipartite graph, one graph for all ranks; random "
+                            "N(0,0.01) embeddings)"),
         "config": {"workload": workload, "num_users": U, "num_items": I, "num_edges": E, "layers": K, "dim": d_full,
-                   "chunk": plan.chunk, "graphs": 1 if c5 else world,
+                   "chunk": chunk, "graphs": 1,
                    "parallelism": (f"feature-sharded over {world} GPU(s): {d} columns each, full plan per rank, "
                                    "no collective") if c5 else
-                                  f"replicas: {world} independent graph instance(s), one per GPU, no collective"},
+                                  (f"row-sharded over {world} GPUs: edge-balanced destination row ranges, the whole "
+                                   f"table on every rank, 2 block all_gathers (RCCL) per exchanged layer, each "
+                                   f"overlapped with the other half-layer; bitwise the 1-GPU result" if sharded else
+                                   "single GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": (f"k_spmm_vec<{kernel_lpr(d)},sliced> (lgcn_spmm_run, {n_slices} source-slice "
-                                f"launches per layer)" if n_slices > 1 else
-                                f"k_spmm_vec<{kernel_lpr(d)}> (lgcn_spmm_items)"),
-                     "kernel_ms": kernel_ms, "bytes_per_launch": bytes_per_launch,
-                     "launches_per_layer": n_slices},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "basis": basis,
+                     "kernel": (f"k_spmm_vec<{kernel_lpr(d)},sliced> (lgcn_spmm_run_slices, {launches} source-slice "
+                                f"launches per layer)" if sliced else f"k_spmm_vec<{kernel_lpr(d)}> (lgcn_spmm_items)"),
+                     "kernel_ms": kernel_ms, "launches_per_layer": launches,
+                     "compulsory_bytes_per_launch": comp_launch,
+                     "traffic_over_compulsory": (traffic / comp_launch) if traffic else None,
+                     "algorithmic_bytes_per_launch": alg_launch,
+                     "effective_GBps": alg_launch / (kernel_ms * 1e-3) / 1e9},
         "cpu_baseline": None,
     }
+    if exchange is not None:
+        result["exchange"] = {"all_gathers_per_step": 2 * (K - 1),
+                              "MB_received_per_rank_per_step": exchange.bytes / args.steps / 1e6}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not c5:
         result["cpu_baseline"] = cpu_baseline(graph, K, d)
     if rank == 0:

@@ -38,7 +38,7 @@ extern "C" {
 
 typedef void* lgcn_stream_t; /* a hipStream_t; NULL = the null stream */
 
-#define LGCN_ABI_VERSION 1
+#define LGCN_ABI_VERSION 2
 
 #define LGCN_OK 0
 #define LGCN_E_ARG (-1)         /* bad size / null pointer / unsupported argument */
@@ -191,11 +191,14 @@ int lgcn_coalesce_undirected(const int64_t* src, const int64_t* dst, int64_t P, 
  * item per segment with FIRST/LAST flags (an empty row one flag-only item in slice 0). Items are
  * sorted slice-major, longest first; offsets[s] (device int64[S+1]) is slice s's first item.
  * counts = {n_items, n_splits, n_partials, unsorted}: unsorted != 0 if some row's neighbours are
- * not ascending (the chain could not follow CSR order; use the plain schedule). */
+ * not ascending (the chain could not follow CSR order; use the plain schedule).
+ * row_mask (device uint8[N], nullable): only rows with a nonzero mask get items (a rank's owned
+ * destination rows of a row-sharded plan, lgcn_amd/sharded.py); NULL = every row. */
 int lgcn_slice_schedule_workspace_size(int64_t E, int64_t N, int32_t S, int32_t chunk, size_t* bytes,
                                        int64_t* items_cap);
 int lgcn_slice_schedule_build(const int64_t* rowptr, const int32_t* col, int64_t N, int64_t E,
-                              const int64_t* bounds, int32_t S, int32_t chunk, lgcn_item_t* items, int64_t items_cap,
+                              const int64_t* bounds, int32_t S, int32_t chunk, const uint8_t* row_mask,
+                              lgcn_item_t* items, int64_t items_cap,
                               int64_t* offsets, lgcn_split_t* splits, int64_t splits_cap, int64_t* counts,
                               void* ws, size_t ws_bytes, lgcn_stream_t stream);
 
@@ -210,6 +213,17 @@ int lgcn_spmm_run(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t*
                   int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split, float* y, float* acc_lo,
                   float* acc_hi, int64_t acc_split, float* partial, int32_t mode, float div, float mul,
                   lgcn_stream_t stream, float* run);
+
+/* All S slice launches of one layer of a source-sliced schedule in one call (the loop over
+ * lgcn_spmm_run, issued from C so a layer costs one host call): slice sl is items
+ * [slice_offsets[sl], slice_offsets[sl+1]) of `items`; slice_offsets is HOST memory (int64[S+1]).
+ * Hub chunks (dst < 0) write their partial slots of `partial`; lgcn_spmm_combine over the hub rows
+ * finishes them afterwards, as after lgcn_spmm_run. Same reference code as lgcn_spmm. */
+int lgcn_spmm_run_slices(const lgcn_item_t* items, const int64_t* slice_offsets, int32_t S, const int32_t* col,
+                         const float* val, int64_t N, int32_t d, const float* x_lo, const float* x_hi,
+                         int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split, float* y,
+                         float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode, float div,
+                         float mul, lgcn_stream_t stream, float* run);
 
 /* One launch instead of lgcn_spmm's two (item pass + combine), for schedules whose split rows
  * have few chunks (Cluster-GCN batch plans): workgroup s < n_splits sums split row s itself —

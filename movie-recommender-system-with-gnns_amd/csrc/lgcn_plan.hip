@@ -205,7 +205,7 @@ __device__ __forceinline__ void for_each_segment(const int32_t* __restrict__ col
 // segments, chunks (hub: a segment longer than chunk) and items.
 __global__ void k_slice_count(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col, int64_t N,
                               const int64_t* __restrict__ bounds, int S, int32_t chunk,
-                              int64_t* __restrict__ n_items, int32_t* __restrict__ n_part,
+                              const uint8_t* __restrict__ row_mask, int64_t* __restrict__ n_items, int32_t* __restrict__ n_part,
                               int32_t* __restrict__ n_split, int32_t* __restrict__ unsorted) {
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
@@ -215,6 +215,12 @@ __global__ void k_slice_count(const int64_t* __restrict__ rowptr, const int32_t*
         for (int64_t e = beg + 1 + lane; e < end; e += 64) bad |= col[e] < col[e - 1];
         if (__any(bad) && lane == 0) atomicOr(unsorted, 1);
         if (lane != 0) continue;
+        if (row_mask != nullptr && row_mask[i] == 0) {  // not scheduled (another rank's row)
+            n_items[i] = 0;
+            n_part[i] = 0;
+            n_split[i] = 0;
+            continue;
+        }
         if (end == beg) {
             n_items[i] = 1;
             n_part[i] = 0;
@@ -237,6 +243,7 @@ __global__ void k_slice_count(const int64_t* __restrict__ rowptr, const int32_t*
 
 __global__ void k_slice_fill(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col, int64_t N,
                              const int64_t* __restrict__ bounds, int S, int32_t chunk,
+                             const uint8_t* __restrict__ row_mask,
                              const int64_t* __restrict__ n_items, const int64_t* __restrict__ item_off,
                              const int32_t* __restrict__ n_part, const int32_t* __restrict__ part_off,
                              const int32_t* __restrict__ n_split, const int32_t* __restrict__ split_off,
@@ -258,7 +265,9 @@ __global__ void k_slice_fill(const int64_t* __restrict__ rowptr, const int32_t* 
             idx[o] = static_cast<int32_t>(o);
             ++o;
         };
-        if (end == beg) {
+        if (row_mask != nullptr && row_mask[i] == 0) {
+            // no items
+        } else if (end == beg) {
             emit(beg, kSliceFirst | kSliceLast, static_cast<int32_t>(i), 0, 0);
         } else {
             const bool hub = n_part[i] > 0;
@@ -572,7 +581,8 @@ int lgcn_slice_schedule_workspace_size(int64_t E, int64_t N, int32_t S, int32_t 
 }
 
 int lgcn_slice_schedule_build(const int64_t* rowptr, const int32_t* col, int64_t N, int64_t E,
-                              const int64_t* bounds, int32_t S, int32_t chunk, lgcn_item_t* items, int64_t items_cap,
+                              const int64_t* bounds, int32_t S, int32_t chunk, const uint8_t* row_mask,
+                              lgcn_item_t* items, int64_t items_cap,
                               int64_t* offsets, lgcn_split_t* splits, int64_t splits_cap, int64_t* counts,
                               void* ws, size_t ws_bytes, lgcn_stream_t stream) {
     if (!rowptr || !bounds || !counts || !offsets || N <= 0 || E < 0 || S < 1 || S > 250 || chunk < 1 ||
@@ -608,7 +618,8 @@ int lgcn_slice_schedule_build(const int64_t* rowptr, const int32_t* col, int64_t
     // counts[3] = 1 if some row's neighbours are not ascending (the caller falls back)
     if (int rc = check_hip(hipMemsetAsync(counts, 0, 4 * sizeof(int64_t), s), "memset counts")) return rc;
     const unsigned g = grid_for(N, kBlock, 8192);
-    k_slice_count<<<grid_for(N * 64, kBlock, 8192), kBlock, 0, s>>>(rowptr, col, N, bounds, S, chunk, n_items, n_part,
+    k_slice_count<<<grid_for(N * 64, kBlock, 8192), kBlock, 0, s>>>(rowptr, col, N, bounds, S, chunk, row_mask,
+                                                                     n_items, n_part,
                                                                      n_split,
                                        reinterpret_cast<int32_t*>(counts + 3));
     if (int rc = check_launch("k_slice_count")) return rc;
@@ -622,7 +633,7 @@ int lgcn_slice_schedule_build(const int64_t* rowptr, const int32_t* col, int64_t
     if (int rc = check_launch("k_fill_u32")) return rc;
     k_fill_u32<<<grid_for(cap, kBlock, 8192), kBlock, 0, s>>>(reinterpret_cast<uint32_t*>(i_in), cap, 0u);
     if (int rc = check_launch("k_fill_u32")) return rc;
-    k_slice_fill<<<g, kBlock, 0, s>>>(rowptr, col, N, bounds, S, chunk, n_items, item_off, n_part, part_off, n_split,
+    k_slice_fill<<<g, kBlock, 0, s>>>(rowptr, col, N, bounds, S, chunk, row_mask, n_items, item_off, n_part, part_off, n_split,
                                       split_off, raw, k_in, i_in, splits, counts);
     if (int rc = check_launch("k_slice_fill")) return rc;
     t = cub_bytes;

@@ -550,6 +550,23 @@ int lgcn_spmm_run(LGCN_SPMM_PARAMS, float* run) {
     if (!run) return fail(LGCN_E_ARG, "lgcn_spmm_run: null running-sum buffer");
     return spmm_impl(LGCN_SPMM_ARGS, PASS_ITEMS, run);
 }
+int lgcn_spmm_run_slices(const lgcn_item_t* items, const int64_t* slice_offsets, int32_t S, const int32_t* col,
+                         const float* val, int64_t N, int32_t d, const float* x_lo, const float* x_hi,
+                         int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split, float* y,
+                         float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode, float div,
+                         float mul, lgcn_stream_t stream, float* run) {
+    if (!run || S < 0 || (S > 0 && (!items || !slice_offsets)))
+        return fail(LGCN_E_ARG, "lgcn_spmm_run_slices: bad args");
+    for (int32_t sl = 0; sl < S; ++sl) {
+        const int64_t b = slice_offsets[sl], n = slice_offsets[sl + 1] - b;
+        if (b < 0 || n < 0) return fail(LGCN_E_ARG, "lgcn_spmm_run_slices: offsets not ascending at slice %d", sl);
+        if (n == 0) continue;
+        if (int rc = spmm_impl(items + b, n, nullptr, 0, col, val, N, d, x_lo, x_hi, x_split, e_lo, e_hi, e_split, y,
+                               acc_lo, acc_hi, acc_split, partial, mode, div, mul, stream, PASS_ITEMS, run))
+            return rc;
+    }
+    return LGCN_OK;
+}
 int lgcn_spmm_blocksplit(LGCN_SPMM_PARAMS, const lgcn_item_t* chunks) {
     return spmm_impl(LGCN_SPMM_ARGS, PASS_BSPLIT, nullptr, chunks);
 }

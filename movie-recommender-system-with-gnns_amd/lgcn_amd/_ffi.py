@@ -23,6 +23,7 @@ EPI_SCALE = 5
 
 ITEM_BYTES = 16   # lgcn_item_t {int64 beg; int32 len; int32 dst}
 SPLIT_BYTES = 16  # lgcn_split_t {int32 row, pbeg, pcnt, pad}
+ABI_VERSION = 2  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
 
 _lib = None
 
@@ -53,6 +54,9 @@ _SIGS = {
     "lgcn_spmm_run": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
                        _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp],
                       ctypes.c_int),
+    "lgcn_spmm_run_slices": ([_vp, _vp, _i32, _vp, _vp, _i64, _i32,
+                              _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp],
+                             ctypes.c_int),
     "lgcn_spmm_blocksplit": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
                               _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp],
                              ctypes.c_int),
@@ -81,8 +85,8 @@ _SIGS = {
     "lgcn_select_topk": ([_vp, _vp, _vp, _i32, _i32, _i32, _i64, _i64, _i64, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_legacy_choice": ([_vp, _vp, _i64, _i64, _i64, _vp], ctypes.c_int),
     "lgcn_slice_schedule_workspace_size": ([_i64, _i64, _i32, _i32, _vp, _vp], ctypes.c_int),
-    "lgcn_slice_schedule_build": ([_vp, _vp, _i64, _i64, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _sz,
-                                   _vp], ctypes.c_int),
+    "lgcn_slice_schedule_build": ([_vp, _vp, _i64, _i64, _vp, _i32, _i32, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp,
+                                   _sz, _vp], ctypes.c_int),
     "lgcn_coalesce_workspace_size": ([_i64, _i64, _vp], ctypes.c_int),
     "lgcn_coalesce_undirected": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
     "lgcn_flagged_rows_add": ([_vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _i64, _vp], ctypes.c_int),
@@ -120,8 +124,8 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
-    if lib.lgcn_abi_version() != 1:
-        raise LgcnError(f"liblgcn ABI version {lib.lgcn_abi_version()} != 1")
+    if lib.lgcn_abi_version() != ABI_VERSION:
+        raise LgcnError(f"liblgcn ABI version {lib.lgcn_abi_version()} != {ABI_VERSION}")
     if path is None:
         _lib = lib
     return lib

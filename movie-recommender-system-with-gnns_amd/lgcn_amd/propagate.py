@@ -18,8 +18,8 @@ from . import _ffi
 from .plan import CsrDirection, PropagationPlan
 from .sliced import SlicedDirection, spmm_sliced, spmm_sliced_combine
 
-# Optional per-launch timing hook (bench.py): a callable(name) -> context manager that records
-# HIP events around the main propagation kernel on the launching stream.
+# Optional per-launch timing hook (bench.py): a callable(d, n_launches) -> context manager that
+# records HIP events on the launching stream around n_launches item-pass launches.
 _launch_timer = None
 
 
@@ -48,7 +48,7 @@ def spmm(direction, N: int, d: int, x, e, acc, y, mode: int, div: float = 1.0, m
         run = y if y is not None else torch.empty((N, d), dtype=torch.float32, device=acc[0].device)
         if _launch_timer is not None:
             # one bracket around the layer's slice launches (2 events per layer, not per launch)
-            with _launch_timer(d):
+            with _launch_timer(d, direction.n_launches):
                 spmm_sliced(direction, N, d, x, e, acc, y, mode, div, mul, run, partial, stream, combine=False)
             spmm_sliced_combine(direction, N, d, x, e, acc, y, mode, div, mul, partial, stream)
         else:
@@ -65,7 +65,7 @@ def spmm(direction, N: int, d: int, x, e, acc, y, mode: int, div: float = 1.0, m
                 _ffi.ptr(xl), _ffi.ptr(xh), xs, _ffi.ptr(el), _ffi.ptr(eh), es,
                 _ffi.ptr(y), _ffi.ptr(al), _ffi.ptr(ah), as_, None, mode, div, mul, stream, chunks.data_ptr())
         if _launch_timer is not None:
-            with _launch_timer(d):
+            with _launch_timer(d, 1):
                 rc = lib.lgcn_spmm_blocksplit(*args)
         else:
             rc = lib.lgcn_spmm_blocksplit(*args)
@@ -77,7 +77,7 @@ def spmm(direction, N: int, d: int, x, e, acc, y, mode: int, div: float = 1.0, m
             _ffi.ptr(y), _ffi.ptr(al), _ffi.ptr(ah), as_, _ffi.ptr(partial), mode, div, mul, stream)
     if _launch_timer is not None:
         # bracket the item pass (the dominant kernel) alone; the combine pass follows it
-        with _launch_timer(d):
+        with _launch_timer(d, 1):
             rc = lib.lgcn_spmm_items(*args)
         _ffi.check(rc, "lgcn_spmm_items")
         rc = lib.lgcn_spmm_combine(*args)

@@ -1,0 +1,311 @@
+"""Row-sharded full-graph propagation over W GPUs (BASELINE.json's headline
+"edges propagated/sec (K=3, d=64) at 1/2/4/8 GPUs" on configs[1]).
+
+One graph, one K-layer LightGCN forward (reference models/light_gcn.py:28-40), split over W
+ranks by DESTINATION rows; the total work is fixed (strong scaling):
+
+* Ownership. Rank r owns one contiguous range of the user rows and one of the item rows, cut so
+  every rank carries about the same number of in-edges (``balanced_bounds``). Every rank keeps
+  the whole embedding table and the whole graph (it gathers from every source row).
+* Padded layout. Rank r's rows sit at [r*cu, r*cu + n_r) of a padded user block of W*cu rows and
+  at W*cu + [r*ci, r*ci + m_r) of a padded item block of W*ci rows (cu, ci = the largest range),
+  so one layer's rows of every rank land with one ``all_gather_into_tensor`` per block (equal
+  chunks, no copy). Node ids are remapped by ``RowShards.padmap``, which is strictly increasing:
+  every row keeps its neighbours in the same order, so its sum is the same chain of additions as
+  on one GPU. The source-slice bounds of the one-GPU schedule are mapped the same way, so hub
+  rows are cut into the same chunks: the sharded result is BITWISE the one-GPU result.
+* Exchange overlapped with compute (bipartite graphs: every edge joins a user and an item).
+  User rows gather only item rows and item rows only user rows, so a layer splits into two
+  halves that share no row: A = the user-source slices (writes the item rows), B = the
+  item-source slices (writes the user rows). Layer k runs A,B (k odd) or B,A (k even): each half
+  reads the block whose all_gather was started first, and the block a half writes is all-gathered
+  (RCCL, on a side stream) while the next half computes. Only layers 1..K-1 are exchanged; the
+  final embedding stays row-sharded (each rank holds its own rows of the output).
+* Non-bipartite graphs run each layer as one piece and exchange both blocks after it.
+
+Host-side logic (``RowShards``, ``propagate_forward_sharded``) is device-agnostic so the gloo
+CPU tests can drive the layer/exchange schedule; the kernels are the same lgcn_spmm* launches as
+the one-GPU path (lgcn_amd.propagate.spmm).
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+import torch
+
+from . import _ffi
+
+ROW_COST = 4  # a row's epilogue (acc/e/y traffic) costs about as much as this many gathered edges
+
+
+def balanced_bounds(weight: np.ndarray, W: int) -> np.ndarray:
+    """W+1 cut points over len(weight) rows: contiguous ranges of about equal weight."""
+    weight = np.asarray(weight, dtype=np.float64)
+    cs = np.concatenate([[0.0], np.cumsum(weight)])
+    cuts = np.searchsorted(cs, cs[-1] * np.arange(1, W) / W, side="left")
+    out = np.concatenate([[0], cuts, [weight.size]]).astype(np.int64)
+    return np.maximum.accumulate(out)
+
+
+@dataclasses.dataclass
+class RowShards:
+    """Ownership of the N = U + I destination rows by W ranks, and the padded id layout."""
+
+    W: int
+    U: int
+    I: int
+    ub: np.ndarray  # int64[W+1] user-row bounds (ids 0..U)
+    ib: np.ndarray  # int64[W+1] item-row bounds (item-local ids 0..I)
+
+    @classmethod
+    def build(cls, in_degree: np.ndarray, U: int, W: int) -> "RowShards":
+        deg = np.asarray(in_degree, dtype=np.int64)
+        I = deg.size - U
+        if U < 0 or I < 0 or W < 1:
+            raise ValueError(f"bad shard request U={U} N={deg.size} W={W}")
+        return cls(W, U, I, balanced_bounds(deg[:U] + ROW_COST, W), balanced_bounds(deg[U:] + ROW_COST, W))
+
+    @property
+    def N(self) -> int:
+        return self.U + self.I
+
+    @property
+    def cu(self) -> int:
+        return int(np.diff(self.ub).max()) if self.W else 0
+
+    @property
+    def ci(self) -> int:
+        return int(np.diff(self.ib).max()) if self.W else 0
+
+    @property
+    def side(self) -> int:
+        """First padded id of the item block."""
+        return self.W * self.cu
+
+    @property
+    def NP(self) -> int:
+        return self.W * (self.cu + self.ci)
+
+    def padmap(self) -> np.ndarray:
+        """int64[N]: original node id -> padded id (strictly increasing)."""
+        out = np.empty(self.N, dtype=np.int64)
+        for r in range(self.W):
+            a, b = self.ub[r], self.ub[r + 1]
+            out[a:b] = r * self.cu + np.arange(b - a)
+            a, b = self.ib[r], self.ib[r + 1]
+            out[self.U + a:self.U + b] = self.side + r * self.ci + np.arange(b - a)
+        return out
+
+    def user_rows(self, r: int) -> tuple[int, int]:
+        lo = r * self.cu
+        return lo, lo + int(self.ub[r + 1] - self.ub[r])
+
+    def item_rows(self, r: int) -> tuple[int, int]:
+        lo = self.side + r * self.ci
+        return lo, lo + int(self.ib[r + 1] - self.ib[r])
+
+    def block(self, b: str) -> tuple[int, int]:
+        """(first padded row, rows per rank) of block 'u' (users) or 'i' (items)."""
+        return (0, self.cu) if b == "u" else (self.side, self.ci)
+
+    def owned_mask(self, r: int, blocks: str = "ui") -> np.ndarray:
+        m = np.zeros(self.NP, dtype=np.uint8)
+        if "u" in blocks:
+            a, b = self.user_rows(r)
+            m[a:b] = 1
+        if "i" in blocks:
+            a, b = self.item_rows(r)
+            m[a:b] = 1
+        return m
+
+    def pad_bounds(self, bounds) -> list[int]:
+        """Source-slice bounds (original ids, 0..N) in padded ids: each source keeps its slice."""
+        pm = self.padmap()
+        return [int(pm[b]) if b < self.N else self.NP for b in bounds]
+
+    def to_padded(self, user_w: torch.Tensor, item_w: torch.Tensor) -> torch.Tensor:
+        """The [NP, d] padded table of (user_w, item_w); padding rows are zero."""
+        d = user_w.shape[1]
+        out = torch.zeros((self.NP, d), dtype=user_w.dtype, device=user_w.device)
+        pm = torch.from_numpy(self.padmap()).to(user_w.device)
+        out[pm[: self.U]] = user_w
+        out[pm[self.U:]] = item_w
+        return out
+
+    def from_padded(self, xp: torch.Tensor) -> torch.Tensor:
+        """[N, d] rows of a padded table, in original id order."""
+        return xp[torch.from_numpy(self.padmap()).to(xp.device)]
+
+
+@dataclasses.dataclass
+class Half:
+    """One piece of a layer: the schedule of the rows it writes and the blocks it reads/writes."""
+
+    direction: object  # CsrDirection | SlicedDirection (device) or a test stand-in
+    reads: str         # 'u', 'i' or 'ui'
+    writes: str
+    partial: torch.Tensor | None = None
+
+
+class ShardedPlan:
+    """Rank `rank`'s propagation plan of a row-sharded graph: the whole (padded) CSR with gcn_norm
+    weights from the whole graph's degrees, and the schedules of its own rows, per half."""
+
+    def __init__(self, edge_index: torch.Tensor, shards: RowShards, rank: int, d: int, chunk: int | None = None):
+        from .plan import DEFAULT_CHUNK, CsrDirection, _build_direction, _schedule, slice_bytes_for
+        from .sliced import build_sliced, slice_bounds
+
+        _ffi.require_device(edge_index, "ShardedPlan")
+        if edge_index.dim() != 2 or edge_index.shape[0] != 2 or edge_index.dtype != torch.int64:
+            raise ValueError("edge_index must be int64 [2, E]")
+        self.shards, self.rank, self.d = shards, int(rank), int(d)
+        self.chunk = int(chunk or DEFAULT_CHUNK)
+        dev = edge_index.device
+        self.device = dev
+        N, U, NP, side = shards.N, shards.U, shards.NP, shards.side
+        E = int(edge_index.shape[1])
+        self.num_edges = E
+        if E and (int(edge_index.min()) < 0 or int(edge_index.max()) >= N):
+            raise IndexError(f"edge_index holds node ids outside [0, {N})")
+        pm = torch.from_numpy(shards.padmap()).to(dev)
+        eip = pm[edge_index]
+        self.bipartite = bool(E == 0 or ((edge_index[0] < U) != (edge_index[1] < U)).all().item())
+        stream = _ffi.stream_of(dev)
+        owned = torch.from_numpy(shards.owned_mask(rank)).to(dev)
+        # the whole graph's CSR over the padded ids (degrees, hence gcn_norm, of the whole graph);
+        # only this rank's rows are scheduled
+        self.fwd, self.dis, _ = _build_direction(eip[1].contiguous(), eip[0].contiguous(), NP, self.chunk, side, None,
+                                                 stream, owned)
+        del eip
+        if self.bipartite:
+            pieces = [("u", "i", torch.from_numpy(shards.owned_mask(rank, "i")).to(dev)),   # A: user sources
+                      ("i", "u", torch.from_numpy(shards.owned_mask(rank, "u")).to(dev))]   # B: item sources
+        else:
+            pieces = [("ui", "ui", owned)]
+        # the one-GPU plan's slicing decision and bounds (lgcn_amd.plan.PropagationPlan.schedule),
+        # mapped to padded ids: the same segments, the same hub chunks
+        sb = slice_bytes_for(N, d)
+        bounds = slice_bounds(N, U, d, sb) if (sb and E) else None
+        if bounds is not None and not (E >= 8 * (len(bounds) - 1) * N or _slice_forced()):
+            bounds = None
+        self.halves: list[Half] = []
+        for reads, writes, mask in pieces:
+            direction = None
+            if bounds is not None:
+                direction = build_sliced(self.fwd, NP, shards.pad_bounds(bounds), self.chunk, mask)
+            if direction is None:
+                f = self.fwd
+                direction = CsrDirection(f.rowptr, f.col, f.eid, f.val,
+                                         *_schedule(f.rowptr, NP, E, self.chunk, side, mask, stream), self.chunk)
+            partial = (torch.empty((direction.n_partials, d), dtype=torch.float32, device=dev)
+                       if direction.n_partials else None)
+            self.halves.append(Half(direction, reads, writes, partial))
+        self.sliced = bounds is not None and all(hasattr(h.direction, "launches") for h in self.halves)
+
+    @property
+    def NP(self) -> int:
+        return self.shards.NP
+
+    def run_half(self, h: Half, x: torch.Tensor, e: torch.Tensor | None, acc: torch.Tensor, y: torch.Tensor | None,
+                 mode: int, div: float, mul: float) -> None:
+        from .propagate import spmm
+
+        NP = self.NP
+        spmm(h.direction, NP, self.d, (x, None, NP), None if e is None else (e, None, NP), (acc, None, NP), y, mode,
+             div, mul, h.partial)
+
+
+def _slice_forced() -> bool:
+    import os
+
+    return os.environ.get("LGCN_SLICE_MB") is not None
+
+
+class BlockExchange:
+    """all_gather of one block (every rank's user rows, or item rows) of a layer output.
+
+    nccl (RCCL over xGMI): ``all_gather_into_tensor`` in place (each rank's chunk is its slice of
+    the output block), issued on a side stream after an event on the compute stream; the caller's
+    stream waits on the returned event only before the half that reads the block.
+    gloo (tests, rehearsal): the same collective through host memory, synchronously."""
+
+    def __init__(self, shards: RowShards, rank: int, group=None):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.shards, self.rank, self.group = shards, rank, group
+        self.nccl = dist.get_backend(group) == "nccl"
+        self.stream = None
+        self.bytes = 0  # received per rank, over the run
+
+    def start(self, buf: torch.Tensor, b: str):
+        lo, c = self.shards.block(b)
+        W = self.shards.W
+        out = buf[lo: lo + W * c]
+        mine = out[self.rank * c:(self.rank + 1) * c]
+        self.bytes += (W - 1) * c * buf.shape[1] * buf.element_size()
+        if self.nccl:
+            if self.stream is None:
+                self.stream = torch.cuda.Stream(buf.device)
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(buf.device))
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ready)
+                self.dist.all_gather_into_tensor(out, mine, group=self.group)
+                done = torch.cuda.Event()
+                done.record(self.stream)
+            return done
+        host = torch.empty((W * c, buf.shape[1]), dtype=buf.dtype)
+        self.dist.all_gather_into_tensor(host, mine.cpu().clone(), group=self.group)
+        out.copy_(host)
+        return None
+
+    def wait(self, handle, device) -> None:
+        if handle is not None:
+            torch.cuda.current_stream(device).wait_event(handle)
+
+
+def propagate_forward_sharded(x0p: torch.Tensor, splan, K: int, exchange: BlockExchange | None) -> torch.Tensor:
+    """out[NP, d] = LightGCN final embedding of this rank's rows (padded ids; the other ranks' rows
+    are not written). x0p: the whole padded layer-0 table (RowShards.to_padded), on every rank."""
+    NP, d = x0p.shape
+    if NP != splan.NP:
+        raise ValueError(f"x0p has {NP} rows, the sharded plan {splan.NP}")
+    dev = x0p.device
+    out = torch.empty((NP, d), dtype=torch.float32, device=dev)
+    div = float(K + 1)
+    mul = float(np.float32(1.0 / (K + 1)))
+    if K == 0:
+        return (x0p / div) * mul
+    bufs = [torch.empty((NP, d), dtype=torch.float32, device=dev) for _ in range(min(2, K - 1))]
+    last_run = torch.empty((NP, d), dtype=torch.float32, device=dev) if splan.sliced else None
+    pending: dict = {}
+    for k in range(1, K + 1):
+        src = x0p if k == 1 else bufs[(k - 2) % 2]
+        dst = bufs[(k - 1) % 2] if k < K else None
+        if K == 1:
+            mode = _ffi.EPI_FINAL_E
+        elif k == 1:
+            mode = _ffi.EPI_INIT
+        elif k < K:
+            mode = _ffi.EPI_ADD
+        else:
+            mode = _ffi.EPI_FINAL_ACC
+        final = mode in (_ffi.EPI_FINAL_E, _ffi.EPI_FINAL_ACC)
+        e = x0p if mode in (_ffi.EPI_INIT, _ffi.EPI_FINAL_E) else None
+        order = splan.halves if k % 2 == 1 else splan.halves[::-1]
+        started: dict = {}
+        for h in order:
+            for b in h.reads:
+                if b in pending:
+                    exchange.wait(pending.pop(b), dev)
+            # sliced schedules use y as the running row sums (the final layer's y is scratch: the
+            # FINAL epilogues never write y)
+            y = dst if dst is not None else last_run
+            splan.run_half(h, src, e, out, y, mode, div if final else 1.0, mul if final else 1.0)
+            if dst is not None and exchange is not None:
+                for b in h.writes:
+                    started[b] = exchange.start(dst, b)
+        pending = started
+    return out

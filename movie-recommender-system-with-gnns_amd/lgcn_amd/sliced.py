@@ -33,6 +33,12 @@ class SlicedDirection:
     n_splits: int
     n_partials: int
     bounds: list            # source-id slice boundaries
+    items: torch.Tensor = None       # all items, slice-major (launches are views of it)
+    host_offsets: object = None      # ctypes int64[S+1]: slice s = items[off[s]:off[s+1]]
+
+    @property
+    def n_launches(self) -> int:
+        return sum(1 for _, n in self.launches if n)
 
     @property
     def col(self):
@@ -57,11 +63,12 @@ def slice_bounds(N: int, U: int, d: int, slice_bytes: int) -> list[int]:
     return sorted(set(out))
 
 
-def build_sliced(f: CsrDirection, N: int, bounds: list[int], chunk: int = 256) -> SlicedDirection | None:
+def build_sliced(f: CsrDirection, N: int, bounds: list[int], chunk: int = 256,
+                 row_mask: torch.Tensor | None = None) -> SlicedDirection | None:
     """The sliced schedule of direction f (lgcn_slice_schedule_build, on the device). None when
     some row's neighbours are not in ascending order (an uncoalesced edge_index): its slice
     segments would not be successive runs of its edge list, so the chain could not follow CSR
-    order — the plain schedule is used then."""
+    order — the plain schedule is used then. row_mask (uint8[N]): schedule only those rows."""
     import ctypes
 
     lib = _ffi.load()
@@ -79,7 +86,7 @@ def build_sliced(f: CsrDirection, N: int, bounds: list[int], chunk: int = 256) -
     counts = torch.zeros(4, dtype=torch.int64, device=dev)
     bnd = torch.tensor(bounds, dtype=torch.int64, device=dev)
     _ffi.check(lib.lgcn_slice_schedule_build(f.rowptr.data_ptr(), _ffi.ptr(f.col), N, E, bnd.data_ptr(), S, chunk,
-                                             items.data_ptr(), cap.value, offsets.data_ptr(), splits.data_ptr(),
+                                             _ffi.ptr(row_mask), items.data_ptr(), cap.value, offsets.data_ptr(), splits.data_ptr(),
                                              splits.shape[0], counts.data_ptr(), ws.data_ptr(), ws.numel(), stream),
                "lgcn_slice_schedule_build")
     host = torch.cat([counts, offsets]).cpu().tolist()  # one read-back per plan
@@ -89,7 +96,8 @@ def build_sliced(f: CsrDirection, N: int, bounds: list[int], chunk: int = 256) -
     if unsorted:
         return None
     launches = [(items[off[s]:off[s + 1]], off[s + 1] - off[s]) for s in range(S)]
-    return SlicedDirection(f, launches, splits, n_splits, n_partials, list(bounds))
+    return SlicedDirection(f, launches, splits, n_splits, n_partials, list(bounds), items,
+                           (ctypes.c_int64 * (S + 1))(*off))
 
 
 def _tail(sd: SlicedDirection, N, d, x, e, acc, y, mode, div, mul, partial, stream):
@@ -103,19 +111,20 @@ def _tail(sd: SlicedDirection, N, d, x, e, acc, y, mode, div, mul, partial, stre
 def spmm_sliced(sd: SlicedDirection, N: int, d: int, x, e, acc, y, mode: int, div: float, mul: float,
                 run: torch.Tensor, partial: torch.Tensor | None, stream: int, combine: bool = True,
                 timer=None) -> None:
-    """One layer over a sliced direction: one lgcn_spmm_run per slice, then the hub combine.
-    timer (bench.py): a callable(d) -> context manager bracketing each slice launch."""
+    """One layer over a sliced direction: one item-pass launch per slice (all issued by one
+    lgcn_spmm_run_slices call), then the hub combine. timer (bench.py): a callable(d) -> context
+    manager bracketing the layer's slice launches."""
     lib = _ffi.load()
-    tail = _tail(sd, N, d, x, e, acc, y, mode, div, mul, partial, stream)
-    for items, n in sd.launches:
-        if n == 0:
-            continue
+    if sd.n_launches:
+        # every slice launch of the layer from one host call (lgcn_spmm_run_slices loops in C)
+        tail = _tail(sd, N, d, x, e, acc, y, mode, div, mul, partial, stream)
+        args = (sd.items.data_ptr(), sd.host_offsets, len(sd.launches), *tail, run.data_ptr())
         if timer is not None:
             with timer(d):
-                rc = lib.lgcn_spmm_run(items.data_ptr(), n, None, 0, *tail, run.data_ptr())
+                rc = lib.lgcn_spmm_run_slices(*args)
         else:
-            rc = lib.lgcn_spmm_run(items.data_ptr(), n, None, 0, *tail, run.data_ptr())
-        _ffi.check(rc, "lgcn_spmm_run")
+            rc = lib.lgcn_spmm_run_slices(*args)
+        _ffi.check(rc, "lgcn_spmm_run_slices")
     if combine:
         spmm_sliced_combine(sd, N, d, x, e, acc, y, mode, div, mul, partial, stream)
 

@@ -81,12 +81,18 @@ def bipartite(num_users: int, num_items: int, num_pairs: int, seed: int = 0, **k
     return BipartiteGraph(num_users, num_items, undirected_from_pairs(u, i, num_users, num_items))
 
 
+# user-activity skew of the ML-25M-shaped graph: calibrated so the heaviest user holds ~3e4
+# rating>=4 pairs (seed 0: user max 31,703, median 35; item max 58,571, median 62)
+ML25M_USER_ALPHA = 0.82
+ML25M_USER_OFFSET = 2.0
+
+
 def ml25m_shaped(seed: int = 0, scale: float = 1.0) -> BipartiteGraph:
     """The C2 graph (scale=1): ML-25M-shaped, E ≈ 2.49e7 directed edges."""
     U = max(2, int(ML25M_USERS * scale))
     I = max(2, int(ML25M_ITEMS * scale))
     P = max(1, int(ML25M_PAIRS * scale))
-    return bipartite(U, I, P, seed)
+    return bipartite(U, I, P, seed, user_alpha=ML25M_USER_ALPHA, user_offset=ML25M_USER_OFFSET)
 
 
 def planted_bipartite(num_users: int, num_items: int, communities: int, degree: int = 20, p_in: float = 0.8,

@@ -83,14 +83,15 @@ class OracleLightGCN(nn.Module):
 
 
 def time_reference_forward(user_w: torch.Tensor, item_w: torch.Tensor, edge_index: torch.Tensor, K: int,
-                           reps: int = 3) -> float:
+                           reps: int = 3, warmup: bool = True) -> float:
     """Median seconds of the reference CPU op sequence for one K-layer forward (no autograd),
-    including gcn_norm per layer exactly as LGConv does."""
+    including gcn_norm per layer exactly as LGConv does. warmup=False times the
+    first run too (for multi-second forwards, where one untimed run would double the cost)."""
     import time
 
     times = []
     with torch.no_grad():
-        for _ in range(reps + 1):
+        for _ in range(reps + (1 if warmup else 0)):
             t0 = time.perf_counter()
             emb = torch.cat([user_w, item_w])
             embs = [emb]
@@ -100,7 +101,7 @@ def time_reference_forward(user_w: torch.Tensor, item_w: torch.Tensor, edge_inde
             out = 1 / (K + 1) * torch.mean(torch.stack(embs, dim=1), dim=1)
             torch.split(out, [user_w.shape[0], item_w.shape[0]])
             times.append(time.perf_counter() - t0)
-    times = sorted(times[1:])
+    times = sorted(times[1:] if warmup else times)
     return times[len(times) // 2]
 
 

@@ -8,15 +8,18 @@ Two anchors, because the reference's hot path is split across two places:
    bpr_loss (+ autograd grads), get_triplets_indices under a fixed torch seed,
    compute_recall_at_k under a fixed numpy seed, one train() epoch over three cluster batches
    with Adam(1e-3) + clip(1) (post-step weights), and evaluate() (loss, Recall@100).
-   The model those harness functions drive is the CPU restatement of reference
-   models/light_gcn.py (oracle/lgconv_torch.py::OracleLightGCN), because that file imports
-   torch_geometric, which is absent here (an ordinary ModuleNotFoundError).
+   The model those harness functions drive is the reference's own LightGCN class (below).
 
-2. lgconv_cases.npz — LightGCN forward/backward through PyG 2.4.0's LGConv op sequence
-   (gcn_norm: scatter_add_ of ones, pow_(-0.5), masked_fill_; propagate: index_select, mul,
-   scatter_add_) executed with torch CPU primitives (oracle/lgconv_torch.py), on the
-   reference's own toy graph (models/light_gcn.py:68-73, with its import-time seed 0 init) and
-   on seeded reference-shaped graphs: symmetric, 90 % directed subsample (Q3), shuffled union,
+2. lgconv_cases.npz — forward/backward of the reference's OWN LightGCN class: reference
+   models/light_gcn.py:13-40 is loaded unmodified from /root/reference with its one missing
+   import, ``torch_geometric.nn.LGConv`` (PyG 2.4.0, absent here: an ordinary
+   ModuleNotFoundError, SURVEY.md §8c), supplied IN MEMORY by oracle/lgconv_torch.py::OracleLGConv
+   — PyG 2.4.0's LGConv op sequence (gcn_norm: scatter_add_ of ones, pow_(-0.5), masked_fill_;
+   propagate: index_select, mul, scatter_add_) on torch CPU primitives. So the layer-stack mean
+   (Q1), cat/split, the import-time seed and the N(0, 0.01) init are the reference's own code;
+   only the LGConv arithmetic is a restatement (of a named third-party algorithm). Cases: the
+   reference's own toy graph (models/light_gcn.py:68-73, seed-0 init, K=4 default) and seeded
+   reference-shaped graphs: symmetric, 90 % directed subsample (Q3), shuffled union,
    hub-skewed, isolated nodes, and the C1 config (K=2, d=64, 50k edges). Gradients by autograd.
    CSR anchors: torch.sort(stable=True) order of edges by target and by source.
 
@@ -48,18 +51,50 @@ class Batch:
         return self
 
 
+def reference_lightgcn():
+    """The reference's LightGCN class (models/light_gcn.py), loaded from /root/reference without
+    modification. Its ``from torch_geometric.nn import LGConv`` is served by an in-memory module
+    holding OracleLGConv; nothing is written anywhere (no bytecode, no files)."""
+    import importlib.util
+    import types
+
+    from oracle.lgconv_torch import OracleLGConv
+
+    if not REF.exists():
+        raise SystemExit("/root/reference is not mounted: fixtures can only be made in the build container")
+    saved = {k: sys.modules.get(k) for k in ("torch_geometric", "torch_geometric.nn")}
+    pyg = types.ModuleType("torch_geometric")
+    pyg_nn = types.ModuleType("torch_geometric.nn")
+    pyg_nn.LGConv = OracleLGConv
+    pyg.nn = pyg_nn
+    sys.modules["torch_geometric"], sys.modules["torch_geometric.nn"] = pyg, pyg_nn
+    try:
+        spec = importlib.util.spec_from_file_location("ref_light_gcn", REF / "models" / "light_gcn.py")
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    return mod.LightGCN
+
+
 def lgconv_cases():
     import torch
 
     import graphs
     from lgcn_amd import synth
-    from oracle.lgconv_torch import OracleLightGCN, gcn_norm_torch
+    from oracle.lgconv_torch import gcn_norm_torch
+
+    RefLightGCN = reference_lightgcn()
 
     cases = {}
 
     def run(name, U, I, ei, K, d, weights=None, seed=0):
         torch.manual_seed(0)
-        m = OracleLightGCN(U, I, num_layers=K, dim_h=d)
+        m = RefLightGCN(U, I, num_layers=K, dim_h=d)
         if weights is not None:
             with torch.no_grad():
                 m.user_embedding.weight.copy_(torch.from_numpy(weights[0]))
@@ -108,8 +143,8 @@ def harness():
     import train_test as ref_tt  # reference utils/train_test.py
 
     import graphs
-    from oracle.lgconv_torch import OracleLightGCN
 
+    RefLightGCN = reference_lightgcn()
     out = {}
     # --- bpr_loss + grads
     rng = np.random.default_rng(21)
@@ -151,7 +186,7 @@ def harness():
         m = (part[train_ei[0]] == p) & (part[train_ei[1]] == p)
         batches.append(np.ascontiguousarray(train_ei[:, m]))
     torch.manual_seed(0)
-    model = OracleLightGCN(U, I, num_layers=3, dim_h=64)
+    model = RefLightGCN(U, I, num_layers=3, dim_h=64)
     out["train_init_user_w"] = model.user_embedding.weight.detach().numpy().copy()
     out["train_init_item_w"] = model.item_embedding.weight.detach().numpy().copy()
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)

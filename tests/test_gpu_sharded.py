@@ -1,0 +1,129 @@
+"""Row-sharded propagation (lgcn_amd.sharded) with the HIP kernels: the sharded K-layer forward is
+BITWISE the one-GPU forward (lgcn_amd.propagate_forward over PropagationPlan(side_split=U)),
+every rank's rows, for the plain and the source-sliced schedules, with hub rows cut into chunks.
+
+W = 1 runs in this process; W = 2 runs two ranks on the one GPU of the box over gloo (the block
+all_gather goes through host memory; the 8-GPU RCCL run is bench.py --gpus N)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+# (graph, K, d, chunk, LGCN_SLICE_MB or None)
+CASES = {
+    "ml25m5_plain": ("ml25m", 3, 64, 256, None),
+    "ml25m5_sliced": ("ml25m", 3, 64, 64, "0.7"),
+    "hub_sliced": ("hub", 4, 32, 16, "0.05"),
+    "sub_K2_d128": ("sub", 2, 128, 8, None),
+}
+
+
+def _graph(kind):
+    import graphs
+    from lgcn_amd import synth
+
+    if kind == "ml25m":
+        g = synth.ml25m_shaped(seed=5, scale=0.05)
+        return g.num_users, g.num_items, g.edge_index
+    if kind == "hub":
+        return graphs.hub(U=3000, I=60)
+    return graphs.subsampled(U=400, I=300, pairs=6000, seed=2)
+
+
+def _reference(dev, case):
+    """One-GPU forward with the same plan settings."""
+    from lgcn_amd import propagate_forward
+    from lgcn_amd.plan import PropagationPlan
+
+    kind, K, d, chunk, slice_mb = CASES[case]
+    U, I, ei = _graph(kind)
+    import graphs
+
+    uw, iw = graphs.embeddings(U, I, d, seed=K + d)
+    plan = PropagationPlan(torch.from_numpy(ei).to(dev), U + I, chunk, side_split=U)
+    out = propagate_forward(torch.from_numpy(uw).to(dev), torch.from_numpy(iw).to(dev), plan, K)
+    return U, I, ei, uw, iw, out.cpu().numpy(), plan.schedule("fwd", d)
+
+
+def _sharded(dev, case, world, rank):
+    from lgcn_amd.sharded import BlockExchange, RowShards, ShardedPlan, propagate_forward_sharded
+
+    kind, K, d, chunk, slice_mb = CASES[case]
+    U, I, ei = _graph(kind)
+    import graphs
+
+    uw, iw = graphs.embeddings(U, I, d, seed=K + d)
+    shards = RowShards.build(np.bincount(ei[1], minlength=U + I), U, world)
+    splan = ShardedPlan(torch.from_numpy(ei).to(dev), shards, rank, d, chunk)
+    x0p = shards.to_padded(torch.from_numpy(uw).to(dev), torch.from_numpy(iw).to(dev))
+    ex = BlockExchange(shards, rank) if world > 1 else None
+    out = propagate_forward_sharded(x0p, splan, K, ex).cpu().numpy()
+    a, b = shards.user_rows(rank)
+    c, e = shards.item_rows(rank)
+    return shards, splan, out[a:b], out[c:e]
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_sharded_w1_bitwise(gpu, monkeypatch, case):
+    slice_mb = CASES[case][4]
+    if slice_mb:
+        monkeypatch.setenv("LGCN_SLICE_MB", slice_mb)
+    U, I, ei, uw, iw, ref, sched = _reference(gpu, case)
+    shards, splan, ou, oi = _sharded(gpu, case, 1, 0)
+    assert shards.NP == U + I and splan.sliced == hasattr(sched, "launches")
+    assert splan.bipartite and len(splan.halves) == 2
+    assert np.array_equal(ou, ref[:U]) and np.array_equal(oi, ref[U:])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, case, out_dir):
+    import sys
+
+    from conftest import PKG, ROOT
+    sys.path[:0] = [str(PKG), str(ROOT), str(ROOT / "tests")]
+    import torch.distributed as dist
+
+    slice_mb = CASES[case][4]
+    if slice_mb:
+        os.environ["LGCN_SLICE_MB"] = slice_mb
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    shards, splan, ou, oi = _sharded(dev, case, world, rank)
+    np.save(os.path.join(out_dir, f"u{rank}.npy"), ou)
+    np.save(os.path.join(out_dir, f"i{rank}.npy"), oi)
+    np.save(os.path.join(out_dir, f"n{rank}.npy"),
+            np.array([sum(getattr(h.direction, "n_splits", 0) for h in splan.halves), int(splan.sliced)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_sharded_two_ranks_bitwise(gpu, monkeypatch, tmp_path, case):
+    slice_mb = CASES[case][4]
+    if slice_mb:
+        monkeypatch.setenv("LGCN_SLICE_MB", slice_mb)
+    U, I, ei, uw, iw, ref, sched = _reference(gpu, case)
+    torch.cuda.synchronize()
+    mp.spawn(_worker, args=(2, _free_port(), case, str(tmp_path)), nprocs=2, join=True)
+    got_u = np.concatenate([np.load(tmp_path / f"u{r}.npy") for r in range(2)])
+    got_i = np.concatenate([np.load(tmp_path / f"i{r}.npy") for r in range(2)])
+    assert np.array_equal(got_u, ref[:U]) and np.array_equal(got_i, ref[U:])
+    meta = [np.load(tmp_path / f"n{r}.npy") for r in range(2)]
+    assert all(int(m[1]) == int(hasattr(sched, "launches")) for m in meta)
+    # the hub rows (chunked in both) are split between the ranks, none lost
+    assert sum(int(m[0]) for m in meta) == sched.n_splits

@@ -8,14 +8,9 @@ import torch
 
 import graphs
 from oracle import c_oracle
+from parity import assert_rows_close
 
 pytestmark = pytest.mark.gpu
-
-RTOL = 1e-5
-
-
-def _rel(a, b):
-    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
 
 
 def _plan(ei, N, dev, U, chunk):
@@ -53,11 +48,11 @@ def test_sliced_forward_backward(gpu, force_slices, name, K):
     out = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, K).cpu().numpy()
     ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
     ref = np.concatenate([ru, ri])
-    assert _rel(out, ref) <= RTOL
+    assert_rows_close(out, ref)
     dF = np.random.default_rng(K).standard_normal((N, d)).astype(np.float32)
     gu, gi = propagate_backward(torch.from_numpy(dF).to(gpu), plan, U, K)
     ou, oi = c_oracle.lightgcn_backward(dF, ei, U, K)
-    assert _rel(np.concatenate([gu.cpu().numpy(), gi.cpu().numpy()]), np.concatenate([ou, oi])) <= RTOL
+    assert_rows_close(np.concatenate([gu.cpu().numpy(), gi.cpu().numpy()]), np.concatenate([ou, oi]))
 
 
 @pytest.mark.parametrize("name", ["sym", "subsampled", "hub"])
@@ -77,7 +72,7 @@ def test_sliced_layer_bitwise_on_chained_rows(gpu, force_slices, name, mb):
     ref = c_oracle.lgconv(x, ei, w)
     hub = _hub_mask(plan.schedule("fwd", d), N)
     assert np.array_equal(y[~hub], ref[~hub])
-    assert _rel(y, ref) <= RTOL
+    assert_rows_close(y, ref)
     # transposed operator (autograd backward of one layer)
     gy = lgconv_backward(torch.from_numpy(x).to(gpu), plan).cpu().numpy()
     ref_t = c_oracle.lgconv(x, ei[::-1].copy(), w)
@@ -104,7 +99,7 @@ def test_sliced_widths_and_default_agree(gpu, force_slices, d):
     ok = ~split_plain & ~_hub_mask(sliced.schedule("fwd", d), N)
     assert ok.sum() > N // 2
     assert np.array_equal(a[ok], b[ok])
-    assert _rel(b, a) <= RTOL
+    assert_rows_close(b, a)
 
 
 def test_sliced_schedule_covers_edges_once(gpu, force_slices):
@@ -149,4 +144,4 @@ def test_uncoalesced_edges_fall_back_to_plain_schedule(gpu, force_slices):
     uw, iw = graphs.embeddings(U, I, d, seed=1)
     out = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, 3).cpu().numpy()
     ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, 3)
-    assert _rel(out, np.concatenate([ru, ri])) <= RTOL
+    assert_rows_close(out, np.concatenate([ru, ri]))

@@ -1,0 +1,166 @@
+"""Row-sharded propagation (lgcn_amd.sharded), host logic on CPU, world_size 2 and 3 on gloo.
+
+The HIP kernels need a GPU, so each rank's "kernel" here is a CPU stand-in (CpuShardPlan) that
+computes a layer with the oracle restatement (oracle/lgconv_ref.py) and keeps only the rows the
+rank owns in the half it is asked for. What is under test is the product's host side:
+ownership ranges, the padded id layout, the half order of each layer, the ping-pong buffers,
+the epilogue modes and the block all_gather (BlockExchange over gloo). The sharded output must be
+BITWISE the one-rank oracle forward (tests/test_gpu_sharded.py runs the same with the kernels).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from lgcn_amd import _ffi
+from lgcn_amd.sharded import BlockExchange, Half, RowShards, balanced_bounds, propagate_forward_sharded
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _graph(kind):
+    import graphs
+
+    if kind == "sym":
+        return graphs.sym(seed=4)
+    if kind == "sub":
+        return graphs.subsampled(seed=5)
+    if kind == "hub":
+        return graphs.hub()
+    # not bipartite: add user-user and item-item edges (one piece per layer, both blocks exchanged)
+    U, I, ei = graphs.sym(U=80, I=60, pairs=700, seed=6)
+    rng = np.random.default_rng(6)
+    extra = np.stack([rng.integers(0, U + I, 300), rng.integers(0, U + I, 300)])
+    key = np.unique(np.concatenate([ei[0] * (U + I) + ei[1], extra[0] * (U + I) + extra[1]]))
+    return U, I, np.stack([key // (U + I), key % (U + I)])
+
+
+class CpuShardPlan:
+    """Stand-in for ShardedPlan on CPU: the same halves and blocks, the layer computed by the
+    oracle over the padded edge list (a strictly increasing relabelling, so each row is the same
+    sequential sum), the epilogue applied to the rank's rows of the half only."""
+
+    def __init__(self, ei, shards, rank):
+        from oracle import lgconv_ref as R
+
+        self.R = R
+        self.shards = shards
+        self.NP = shards.NP
+        pm = shards.padmap()
+        self.eip = pm[ei]
+        self.w = R.gcn_norm(self.eip, self.NP)
+        U = shards.U
+        self.bipartite = bool(np.all((ei[0] < U) != (ei[1] < U)))
+        pieces = [("u", "i"), ("i", "u")] if self.bipartite else [("ui", "ui")]
+        self.halves = [Half(None, r, w) for r, w in pieces]
+        self.rows = [np.flatnonzero(shards.owned_mask(rank, w)) for _, w in pieces]
+        self.sliced = False
+        self.log = []
+
+    def run_half(self, h, x, e, acc, y, mode, div, mul):
+        rows = self.rows[self.halves.index(h)]
+        self.log.append((h.reads, h.writes))
+        v = torch.from_numpy(self.R.lgconv(x.numpy(), self.eip, self.w))[rows]
+        if mode == _ffi.EPI_INIT:
+            acc[rows] = e[rows] + v
+        elif mode == _ffi.EPI_ADD:
+            acc[rows] = acc[rows] + v
+        elif mode == _ffi.EPI_FINAL_ACC:
+            acc[rows] = ((acc[rows] + v) / div) * mul
+        elif mode == _ffi.EPI_FINAL_E:
+            acc[rows] = ((e[rows] + v) / div) * mul
+        if y is not None and mode in (_ffi.EPI_INIT, _ffi.EPI_ADD):
+            y[rows] = v
+
+
+def _worker(rank, world, port, kind, K, out_dir):
+    import sys
+
+    from conftest import PKG, ROOT
+    sys.path[:0] = [str(PKG), str(ROOT), str(ROOT / "tests")]
+    import graphs
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    U, I, ei = _graph(kind)
+    deg = np.bincount(ei[1], minlength=U + I)
+    shards = RowShards.build(deg, U, world)
+    plan = CpuShardPlan(ei, shards, rank)
+    uw, iw = graphs.embeddings(U, I, 16, seed=K)
+    x0p = shards.to_padded(torch.from_numpy(uw), torch.from_numpy(iw))
+    ex = BlockExchange(shards, rank)
+    out = propagate_forward_sharded(x0p, plan, K, ex)
+    a, b = shards.user_rows(rank)
+    c, d = shards.item_rows(rank)
+    np.save(os.path.join(out_dir, f"u{rank}.npy"), out[a:b].numpy())
+    np.save(os.path.join(out_dir, f"i{rank}.npy"), out[c:d].numpy())
+    np.save(os.path.join(out_dir, f"log{rank}.npy"), np.array(["".join(x) for x in plan.log]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,world,K", [("sym", 2, 3), ("sub", 2, 3), ("hub", 2, 4), ("sym", 3, 2),
+                                          ("nonbip", 2, 3), ("sub", 2, 1)])
+def test_sharded_equals_single_rank_bitwise(tmp_path, kind, world, K):
+    from oracle import c_oracle
+
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, kind, K, str(tmp_path)), nprocs=world, join=True)
+    import graphs
+
+    U, I, ei = _graph(kind)
+    uw, iw = graphs.embeddings(U, I, 16, seed=K)
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
+    got_u = np.concatenate([np.load(tmp_path / f"u{r}.npy") for r in range(world)])
+    got_i = np.concatenate([np.load(tmp_path / f"i{r}.npy") for r in range(world)])
+    assert np.array_equal(got_u, ru) and np.array_equal(got_i, ri)
+    log = list(np.load(tmp_path / "log0.npy"))
+    if kind != "nonbip":
+        # layer k runs A (reads users, writes items) first when k is odd, B first when k is even
+        expect = [["ui", "iu"] if k % 2 else ["iu", "ui"] for k in range(1, K + 1)]
+        assert log == [x for pair in expect for x in pair]
+    else:
+        assert log == ["uiui"] * K
+
+
+def test_row_shards_layout():
+    U, I, ei = _graph("hub")
+    deg = np.bincount(ei[1], minlength=U + I)
+    for W in (1, 2, 3, 8):
+        s = RowShards.build(deg, U, W)
+        pm = s.padmap()
+        assert np.all(np.diff(pm) > 0)                           # strictly increasing
+        assert pm[U - 1] < s.side <= pm[U]                         # users, then items
+        owned = sum(s.owned_mask(r) for r in range(W))
+        assert owned.max() == 1 and owned.sum() == U + I           # every row owned exactly once
+        assert set(np.flatnonzero(owned)) == set(pm.tolist())
+        # edge-balanced: no rank's users carry much more than its share of the user in-edges
+        eu = [deg[s.ub[r]:s.ub[r + 1]].sum() for r in range(W)]
+        assert max(eu) <= deg[:U].sum() / W + deg[:U].max() + 4 * U / W
+        x = torch.randn(U + I, 8)
+        assert torch.equal(s.from_padded(s.to_padded(x[:U], x[U:])), x)
+        # slice bounds keep every source in its slice
+        bounds = [0, U // 2, U, U + I // 2, U + I]
+        pb = s.pad_bounds(bounds)
+        src = np.arange(U + I)
+        assert np.array_equal(np.searchsorted(bounds, src, side="right"), np.searchsorted(pb, pm[src], side="right"))
+
+
+def test_balanced_bounds():
+    w = np.array([1, 1, 1, 100, 1, 1, 1, 1])
+    b = balanced_bounds(w, 2)
+    assert b[0] == 0 and b[-1] == 8 and np.all(np.diff(b) >= 0)
+    assert list(balanced_bounds(np.ones(10), 5)) == [0, 2, 4, 6, 8, 10]
+    b = balanced_bounds(np.ones(2), 4)  # more ranks than rows: some ranges are empty
+    assert b[0] == 0 and b[-1] == 2 and len(b) == 5 and np.all(np.diff(b) >= 0)
