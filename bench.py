@@ -450,19 +450,11 @@ def run_train(args):
     t0 = time.perf_counter()
     g = synth.ml25m_shaped(seed=0, scale=args.scale)  # one graph, replicated tables (DP)
     U, I, N = g.num_users, g.num_items, g.num_nodes
-    rng = np.random.default_rng(0)
-    perm = rng.permutation(g.num_edges)
-    n_tr = int(0.9 * g.num_edges)
-    train_ei = np.ascontiguousarray(g.edge_index[:, np.sort(perm[:n_tr])])
-    part = cluster.partition_nodes(train_ei, N, args.parts)
-    f_intra = cluster.intra_fraction(train_ei, part)
-    lists = cluster.intra_part_edges(train_ei, part, args.parts)
-    order = np.random.default_rng(1).permutation(args.parts)
+    train_ei = synth.train_split(g.edge_index, 0.9, seed=0)
+    n_tr = train_ei.shape[1]
     q = args.parts_per_batch
-    batches = []
-    for b in range(0, args.parts, q):
-        ei = np.concatenate([lists[p] for p in order[b:b + q]], axis=1)
-        batches.append(Data(edge_index=torch.from_numpy(ei).to(dev), num_nodes=N))
+    _, f_intra, lists = cluster.cluster_batches(train_ei, N, args.parts, q)
+    batches = [Data(edge_index=torch.from_numpy(ei).to(dev), num_nodes=N) for ei in lists]
     log(f"[rank {rank}] train graph E={n_tr} parts={args.parts} f_intra={f_intra:.4f} "
         f"batches={len(batches)} mean E_batch={np.mean([b.edge_index.shape[1] for b in batches]):.0f} "
         f"({time.perf_counter() - t0:.1f} s)")

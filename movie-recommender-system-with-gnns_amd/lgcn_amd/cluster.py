@@ -58,3 +58,18 @@ def intra_fraction(edge_index, part: np.ndarray) -> float:
 
 def part_sizes(part: np.ndarray, num_parts: int) -> np.ndarray:
     return np.bincount(part, minlength=num_parts)
+
+
+def cluster_batches(train_edge_index, num_nodes: int, num_parts: int, parts_per_batch: int,
+                    order_seed: int = 1) -> tuple[np.ndarray, float, list[np.ndarray]]:
+    """The C3/C4 batches: partition the train graph into ``num_parts`` parts, then union the
+    intra-part edges of ``parts_per_batch`` parts per batch, parts taken in a seeded permutation
+    (reference data/dataset_handler.py:273-285 with q parts per DataLoader item).
+    Returns (part[N], intra-part edge fraction, list of [2, E_b] int64 batch edge lists)."""
+    part = partition_nodes(train_edge_index, num_nodes, num_parts)
+    f_intra = intra_fraction(train_edge_index, part)
+    lists = intra_part_edges(train_edge_index, part, num_parts)
+    order = np.random.default_rng(order_seed).permutation(num_parts)
+    batches = [np.ascontiguousarray(np.concatenate([lists[p] for p in order[b:b + parts_per_batch]], axis=1))
+               for b in range(0, num_parts, parts_per_batch)]
+    return part, f_intra, batches

@@ -95,6 +95,14 @@ def ml25m_shaped(seed: int = 0, scale: float = 1.0) -> BipartiteGraph:
     return bipartite(U, I, P, seed, user_alpha=ML25M_USER_ALPHA, user_offset=ML25M_USER_OFFSET)
 
 
+def train_split(edge_index: np.ndarray, frac: float = 0.9, seed: int = 0) -> np.ndarray:
+    """The train share of the directed edges, kept in coalesced order (reference
+    data/dataset_handler.py:160-199: a seeded permutation of edge positions, indices sorted)."""
+    E = edge_index.shape[1]
+    perm = np.random.default_rng(seed).permutation(E)
+    return np.ascontiguousarray(edge_index[:, np.sort(perm[:int(frac * E)])])
+
+
 def planted_bipartite(num_users: int, num_items: int, communities: int, degree: int = 20, p_in: float = 0.8,
                       seed: int = 0) -> tuple[BipartiteGraph, np.ndarray]:
     """A user–item graph with planted taste communities, for judging the partitioner (the

@@ -3,7 +3,10 @@ child process per rank; gloo over one GPU): trains the same Cluster-GCN batches 
 dense FusedAdam after an all_reduce of both gradients, and the row-lazy Adam with the
 row-sparse exchange (eager and hipGraph-replayed) — and saves the final tables and losses.
 
-python tests/dp_exchange_worker.py RANK WORLD PORT OUT CLIP"""
+python tests/dp_exchange_worker.py RANK WORLD PORT OUT CLIP [BATCHES.npz]
+
+With BATCHES.npz (U, I, b0, b1, ...: Cluster-GCN batch edge lists, e.g. C3's) the ranks train
+those batches at d=128 (C4 rehearsal); otherwise a small subsampled graph at d=64."""
 import os
 import sys
 
@@ -37,22 +40,30 @@ def main():
     from lgcn_amd.train_step import FusedTrainStep
     from models.light_gcn import LightGCN
 
-    U, I, ei = graphs.subsampled(U=2000, I=1000, pairs=8000, seed=4)
-    part = C.partition_nodes(ei, U + I, 8)
-    batches = [_Batch(torch.from_numpy(x).to(gpu)) for x in C.intra_part_edges(ei, part, 8)]
+    if len(sys.argv) > 6:
+        import numpy as np
+
+        z = np.load(sys.argv[6])
+        U, I, d = int(z["U"]), int(z["I"]), 128
+        lists = [z[k] for k in sorted((k for k in z.files if k.startswith("b")), key=lambda k: int(k[1:]))]
+    else:
+        U, I, ei = graphs.subsampled(U=2000, I=1000, pairs=8000, seed=4)
+        part = C.partition_nodes(ei, U + I, 8)
+        lists, d = C.intra_part_edges(ei, part, 8), 64
+    batches = [_Batch(torch.from_numpy(x).to(gpu)) for x in lists]
     share = D.rank_share(len(batches), world, rank, seed=0, epoch=0)
     cap = D.exchange_capacity(batches, U)
     res = {}
     for name in ("dense", "lazy", "lazy_graphs"):
         torch.manual_seed(0)
-        m = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
+        m = LightGCN(U, I, num_layers=3, dim_h=d).to(gpu)
         if name == "dense":
             opt = FusedAdam(m.parameters(), lr=1e-2, max_grad_norm=clip, capturable=True)
             step = FusedTrainStep(m, opt, world=world)
         else:
             opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-2,
                               max_grad_norm=clip)
-            ex = D.RowExchange(cap, U + I, 64, gpu, world)
+            ex = D.RowExchange(cap, U + I, d, gpu, world)
             step = FusedTrainStep(m, opt, world=world, lazy=True, exchange=ex, graphs=(name == "lazy_graphs"))
         losses = []
         for i in range(12):
@@ -63,6 +74,7 @@ def main():
         res[name] = {"losses": losses, "user": m.user_embedding.weight.detach().cpu(),
                      "item": m.item_embedding.weight.detach().cpu()}
     res["cap"] = cap
+    res["d"] = d
     torch.save(res, out)
     dist.barrier()
     dist.destroy_process_group()

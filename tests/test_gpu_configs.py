@@ -1,0 +1,259 @@
+"""BASELINE.json's configs beyond the C2 headline, exercised on the GPU against the CPU oracle.
+
+* C3 (configs[2]): the ML-25M-shaped graph, the 90 % train split, the 1024-part partition and one
+  32-part union batch (reference data/dataset_handler.py:256-288), one training step at K=3
+  d=128 (reference utils/train_test.py:86-101): loss, both gradient tables and the post-Adam
+  tables against the reference harness driving the CPU oracle model with the same negatives.
+* C4 (configs[3]): the 2-rank data-parallel exchange (gloo on the one GPU of the box) on C3
+  batches at d=128 against the dense all_reduce step (tests/dp_exchange_worker.py).
+* C5 (configs[4]): the C5 generator at 1/40 scale with C5's schedule (plain items, hub rows cut
+  into chunks, k_spmm_vec<64,1,8>) against the C oracle at K=4 d=256, one layer bitwise on the
+  unsplit rows; and at the FULL C5 size (10M x 1M x 5e8) the size-independent properties of the
+  operator: adjointness of the forward and transposed plans, linearity.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+from oracle import c_oracle
+from parity import assert_rows_close
+
+pytestmark = pytest.mark.gpu
+
+
+class _Batch:
+    def __init__(self, ei):
+        self.edge_index = ei
+
+    def to(self, device):
+        return _Batch(self.edge_index.to(device))
+
+
+@pytest.fixture(scope="module")
+def c3(tmp_path_factory):
+    """The C3 workload as bench.py --workload train builds it (lgcn_amd.cluster.cluster_batches)."""
+    from lgcn_amd import cluster, synth
+
+    g = synth.ml25m_shaped(seed=0)
+    train = synth.train_split(g.edge_index, 0.9, seed=0)
+    _, f_intra, batches = cluster.cluster_batches(train, g.num_nodes, 1024, 32)
+    path = tmp_path_factory.mktemp("c3") / "c3_batches.npz"
+    np.savez(path, U=g.num_users, I=g.num_items, **{f"b{i}": b for i, b in enumerate(batches[:4])})
+    return {"U": g.num_users, "I": g.num_items, "f_intra": f_intra, "batches": batches, "path": str(path)}
+
+
+def test_c3_training_step_matches_oracle(gpu, c3, monkeypatch):
+    from lgcn_amd.optim import RowLazyAdam
+    from lgcn_amd.train_step import FusedTrainStep
+    from models.light_gcn import LightGCN
+    from oracle.lgconv_torch import OracleLightGCN
+    from utils import helpers
+    from utils import train_test as TT
+
+    U, I, K, d = c3["U"], c3["I"], 3, 128
+    ei_np = c3["batches"][0]
+    assert len(c3["batches"]) == 32 and ei_np.shape[1] > 5000, ei_np.shape
+    torch.manual_seed(0)
+    ref = OracleLightGCN(U, I, num_layers=K, dim_h=d)  # the reference's init, on the CPU
+    w0 = {k: v.clone() for k, v in ref.state_dict().items()}
+
+    def hip_model():
+        m = LightGCN(U, I, num_layers=K, dim_h=d).to(gpu)
+        m.load_state_dict(w0)
+        return m
+
+    ei = torch.from_numpy(ei_np).to(gpu)
+    batch = _Batch(ei)
+    # gradients: the fused step's dense gradient tables
+    a = hip_model()
+    step_a = FusedTrainStep(a, None)
+    torch.cuda.manual_seed(7)
+    loss_a = step_a.compute_grads(batch).item()
+    neg = step_a.state(ei).neg.cpu().clone()
+    # post-Adam: the default row-lazy step (clip 1, lr 1e-3) with the same negatives
+    b = hip_model()
+    opt = RowLazyAdam(b.user_embedding.weight.data, b.item_embedding.weight.data, lr=1e-3, max_grad_norm=1)
+    step_b = FusedTrainStep(b, opt, lazy=True)
+    torch.cuda.manual_seed(7)
+    loss_b = step_b.step(batch).item()
+    step_b.sync()
+    torch.cuda.synchronize()
+    assert torch.equal(step_b.state(ei).neg.cpu(), neg)
+
+    # the reference harness on the CPU oracle model, same negatives
+    monkeypatch.setattr(helpers, "sample_negative", lambda pos_idx, num_items, device: neg.to(device))
+    cpu = torch.device("cpu")
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    ropt.zero_grad()
+    loss_r = TT.bpr_loss(*TT.compute_embeddings(ref, _Batch(torch.from_numpy(ei_np)), cpu))
+    loss_r.backward()
+    lr_ = loss_r.item()
+    assert abs(loss_a - lr_) <= 1e-5 * abs(lr_), (loss_a, lr_)
+    assert abs(loss_b - lr_) <= 1e-5 * abs(lr_), (loss_b, lr_)
+    gu_r, gi_r = ref.user_embedding.weight.grad.numpy(), ref.item_embedding.weight.grad.numpy()
+    stats = {}
+    for name, g_h, g_r in (("grad_user", a.user_embedding.weight.grad, gu_r),
+                           ("grad_item", a.item_embedding.weight.grad, gi_r)):
+        stats[name] = assert_rows_close(g_h.cpu().numpy(), g_r, what=f"C3 {name}")
+    torch.nn.utils.clip_grad_norm_(ref.parameters(), max_norm=1)
+    ropt.step()
+    for name, p_h, p_r in (("user", b.user_embedding.weight, ref.user_embedding.weight),
+                           ("item", b.item_embedding.weight, ref.item_embedding.weight)):
+        ph, pr, p0 = p_h.detach().cpu().numpy(), p_r.detach().numpy(), w0[f"{name}_embedding.weight"].numpy()
+        moved_h, moved_r = np.any(ph != p0, axis=1), np.any(pr != p0, axis=1)
+        # the same rows move (touched rows and the step's negatives)
+        assert np.array_equal(moved_h, moved_r), (name, int(moved_h.sum()), int(moved_r.sum()))
+        # Adam's first step moves each weight by ~lr * sign(grad): elements whose gradient is
+        # within rounding of 0 may take the other sign, so bound the fraction that differ
+        diff = np.abs(ph - pr)
+        assert np.mean(diff <= 1e-6) > 0.999 and diff.max() <= 2.1e-3, (name, float(np.mean(diff <= 1e-6)))
+    print(f"C3 batch E={ei_np.shape[1]} f_intra={c3['f_intra']:.4f} loss {loss_a:.7f} vs {lr_:.7f}; "
+          f"grad row-rel {stats}")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_c4_dp2_exchange_on_c3_batches(gpu, c3, tmp_path):
+    """C4 rehearsal: two ranks (gloo, one GPU) train C3 batches at K=3 d=128 three ways; the
+    row-sparse exchange (eager and hipGraph) is bitwise the dense all_reduce + FusedAdam step
+    without clipping, and both ranks end bitwise identical."""
+    port = str(_free_port())
+    worker = str(ROOT / "tests" / "dp_exchange_worker.py")
+    outs = [str(tmp_path / f"r{r}.pt") for r in range(2)]
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
+    procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), "2", port, outs[r], "inf", c3["path"]], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=110)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log
+    res = [torch.load(o, weights_only=True) for o in outs]
+    assert res[0]["d"] == 128
+    for name in ("dense", "lazy", "lazy_graphs"):
+        assert torch.equal(res[0][name]["user"], res[1][name]["user"]), name
+        assert torch.equal(res[0][name]["item"], res[1][name]["item"]), name
+    for r in range(2):
+        dn, lz, lg = res[r]["dense"], res[r]["lazy"], res[r]["lazy_graphs"]
+        assert dn["losses"] == lz["losses"] == lg["losses"]
+        for k in ("user", "item"):
+            assert torch.equal(dn[k], lz[k]) and torch.equal(lz[k], lg[k]), k
+
+
+C5_SCALE = 40
+
+
+@pytest.fixture(scope="module")
+def c5_small(gpu):
+    from lgcn_amd import synth
+
+    U, I, P = synth.C5_USERS // C5_SCALE, synth.C5_ITEMS // C5_SCALE, synth.C5_PAIRS // C5_SCALE
+    ei = synth.bipartite_device(U, I, P, seed=0, device=gpu)
+    return U, I, ei
+
+
+def test_c5_scaled_forward_matches_oracle(gpu, c5_small, monkeypatch):
+    from lgcn_amd import propagate_forward
+    from lgcn_amd.plan import CsrDirection, PropagationPlan
+    from lgcn_amd.propagate import lgconv_forward
+
+    monkeypatch.setenv("LGCN_SLICE_MB", "0")  # C5's schedule: slicing is off above 512 MB tables
+    U, I, ei = c5_small
+    N, K, d = U + I, 4, 256
+    plan = PropagationPlan(ei, N, side_split=U)
+    sched = plan.schedule("fwd", d)
+    assert isinstance(sched, CsrDirection) and sched.n_splits > 0  # hub rows cut into chunks, as at C5
+    rng = np.random.default_rng(0)
+    uw = (rng.standard_normal((U, d)) * 0.01).astype(np.float32)
+    iw = (rng.standard_normal((I, d)) * 0.01).astype(np.float32)
+    out = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, K).cpu().numpy()
+    ei_h = ei.cpu().numpy()
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, ei_h, K)
+    rr, el = assert_rows_close(out, np.concatenate([ru, ri]), what="C5/40 K=4 d=256")
+    # one layer: every unsplit row bitwise the sequential CPU sum
+    x = np.concatenate([uw, iw])
+    y = lgconv_forward(torch.from_numpy(x).to(gpu), plan).cpu().numpy()
+    _, w = c_oracle.gcn_norm(ei_h, N)
+    ref = c_oracle.lgconv(x, ei_h, w)
+    mask = np.ones(N, bool)
+    mask[sched.splits[: sched.n_splits, 0].cpu().numpy()] = False
+    assert np.array_equal(y[mask], ref[mask])
+    rr1, _ = assert_rows_close(y[~mask], ref[~mask], what="C5/40 split rows")
+    print(f"C5/{C5_SCALE}: E={ei.shape[1]} split rows {sched.n_splits}; K=4 row-rel {rr:.2e} "
+          f"(elementwise {el:.2e}); one layer split rows {rr1:.2e}")
+
+
+def _blocked_dot(a, b, rows=1 << 20):
+    s = 0.0
+    for i in range(0, a.shape[0], rows):
+        s += (a[i:i + rows].double() * b[i:i + rows].double()).sum().item()
+    return s
+
+
+def _blocked_norm(a, rows=1 << 20):
+    return _blocked_dot(a, a, rows) ** 0.5
+
+
+def test_c5_fullsize_adjoint_and_linear(gpu):
+    """Full C5 (10M users x 1M items x 5e8 directed edges, d=256): <Â x, y> == <x, Âᵀ y> and
+    Â(2x - 3y) == 2Âx - 3Ây per row, to fp32 rounding."""
+    from lgcn_amd import synth
+    from lgcn_amd.plan import PropagationPlan
+    from lgcn_amd.propagate import lgconv_backward, lgconv_forward
+
+    U, I = synth.C5_USERS, synth.C5_ITEMS
+    N, d = U + I, 256
+    ei = synth.bipartite_device(U, I, synth.C5_PAIRS, seed=0, device=gpu)
+    assert ei.shape[1] == 2 * synth.C5_PAIRS
+    plan = PropagationPlan(ei, N, side_split=U)
+    del ei
+    gen = torch.Generator(device=gpu).manual_seed(1)
+    x = torch.randn(N, d, device=gpu, generator=gen)
+    y = torch.randn(N, d, device=gpu, generator=gen)
+    ax = lgconv_forward(x, plan)
+    aty = lgconv_backward(y, plan)
+    lhs, rhs = _blocked_dot(ax, y), _blocked_dot(x, aty)
+    assert abs(lhs - rhs) <= 1e-5 * _blocked_norm(ax) * _blocked_norm(y), (lhs, rhs)
+    del aty
+    ay = lgconv_forward(y, plan)
+    comb = lgconv_forward(x.mul_(2.0).sub_(y.mul_(3.0)), plan)  # x, y are overwritten from here on
+    del x, y
+    worst = 0.0
+    for i in range(0, N, 1 << 20):
+        a2, a3 = 2.0 * ax[i:i + (1 << 20)], 3.0 * ay[i:i + (1 << 20)]
+        err = (comb[i:i + (1 << 20)] - (a2 - a3)).abs().amax(1)
+        scale = (a2.abs() + a3.abs()).amax(1)
+        assert bool((err <= 1e-5 * scale).all()), "linearity"
+        worst = max(worst, float((err / scale.clamp_min(1e-30)).max()))
+    print(f"C5 full: adjoint |lhs-rhs| = {abs(lhs - rhs):.3e} of {lhs:.6e}; linearity worst row {worst:.2e}")
+
+
+def test_c3_batches_are_symmetric_bipartite(c3):
+    """The C3 batches bench.py times: 32 batches of user-item edges. The 90 % split keeps each
+    direction of a pair independently, so a batch holds both directions of most pairs
+    but not all: the user->item edges (the triplets' users and positives, reference
+    utils/helpers.py:98-99) and the item->user edges differ slightly in count."""
+    U = c3["U"]
+    assert len(c3["batches"]) == 32
+    for b in c3["batches"]:
+        src, dst = b
+        assert ((src < U) != (dst < U)).all()
+        fwd, back = int((src < U).sum()), int((dst < U).sum())
+        assert abs(fwd - back) <= 0.05 * max(fwd, back)

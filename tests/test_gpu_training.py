@@ -337,3 +337,46 @@ def test_recall20_parity_after_training(gpu, cpu_negatives):
         out[name] = rec
     for k in (20, 100):
         assert abs(out["hip"][k] - out["ref"][k]) <= 0.002, (k, out)  # BASELINE.json north star
+
+
+def test_recall_parity_c1_size(gpu, cpu_negatives):
+    """Recall parity at BASELINE configs[0]'s size (U=1000, I=600, 25k pairs -> E = 50k, K=2,
+    d=64; the c1_K2_d64 golden graph): 90/5/5 split, 4 Cluster-GCN parts, one part per step (the
+    reference's batch_size=1), 5 epochs of the reference harness (Adam 1e-3) on the HIP model (GPU)
+    and on the oracle model (CPU) with the same negatives, then Recall@20 / @100 on the 2,500
+    validation edges (reference utils/train_test.py:136-212, same numpy seed). Bar: the north
+    star's +-0.002; the relative difference is printed next to it."""
+    from lgcn_amd import cluster, synth
+    from models.light_gcn import LightGCN
+    from utils import train_test as TT
+
+    g = synth.bipartite(1000, 600, 25_000, seed=11)
+    U, I, E = g.num_users, g.num_items, g.num_edges
+    perm = np.random.default_rng(0).permutation(E)
+    n_tr, n_va = int(0.9 * E), int(0.05 * E)
+    train = np.ascontiguousarray(g.edge_index[:, np.sort(perm[:n_tr])])
+    val = torch.from_numpy(np.ascontiguousarray(g.edge_index[:, np.sort(perm[n_tr:n_tr + n_va])]))
+    _, _, parts = cluster.cluster_batches(train, U + I, 4, 1)
+    parts = [p for p in parts if p.shape[1]]
+    torch.manual_seed(0)
+    ref = OracleLightGCN(U, I, num_layers=2, dim_h=64)
+    hip = LightGCN(U, I, num_layers=2, dim_h=64).to(gpu)
+    hip.load_state_dict(ref.state_dict())
+    out = {}
+    for name, m, dev in (("hip", hip, gpu), ("ref", ref, torch.device("cpu"))):
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        cpu_negatives(31)
+        for _ in range(5):
+            TT.train(m, opt, [_Batch(torch.from_numpy(p)) for p in parts], dev)
+        with torch.no_grad():
+            embs = TT.compute_embeddings(m, _Batch(val).to(dev), dev)
+            rec = {}
+            for k in (20, 100):
+                np.random.seed(5)
+                rec[k] = TT.compute_recall_at_k((embs[1], embs[3], embs[5]), k=k)
+        out[name] = rec
+    for k in (20, 100):
+        d = abs(out["hip"][k] - out["ref"][k])
+        print(f"C1 Recall@{k}: hip {out['hip'][k]:.5f} ref {out['ref'][k]:.5f} |diff| {d:.5f} "
+              f"(rel {d / max(out['ref'][k], 1e-12):.2e}; bar 0.002)")
+        assert d <= 0.002, (k, out)
