@@ -222,6 +222,9 @@ def main():
     ap.add_argument("--workload", choices=["propagate", "train"], default="propagate",
                     help="propagate: C2 headline (default); train: C3/C4 Cluster-GCN training steps")
     ap.add_argument("--parts", type=int, default=1024, help="train: Cluster-GCN parts")
+    ap.add_argument("--graph", choices=["ml25m", "planted"], default="ml25m",
+                    help="train: the ML-25M-shaped random graph (f_intra ~3%%, ~20k-edge batches) or the "
+                         "ML-25M-sized planted-community graph (f_intra ~46%%, ~324k-edge batches)")
     ap.add_argument("--parts-per-batch", type=int, default=32, help="train: parts per step")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for runs; gloo to rehearse N ranks on one GPU")
     ap.add_argument("--torch-adam", action="store_true", help="train: torch Adam + clip_grad_norm_ (reference ops)")
@@ -448,7 +451,10 @@ def run_train(args):
     K = args.layers if args.layers is not None else 3
     d = args.dim if args.dim is not None else 128
     t0 = time.perf_counter()
-    g = synth.ml25m_shaped(seed=0, scale=args.scale)  # one graph, replicated tables (DP)
+    if args.graph == "planted":  # ML-25M-sized with 1024 planted communities: big intra-part batches
+        g, _ = synth.planted_ml25m(1024, scale=args.scale)
+    else:
+        g = synth.ml25m_shaped(seed=0, scale=args.scale)  # one graph, replicated tables (DP)
     U, I, N = g.num_users, g.num_items, g.num_nodes
     train_ei = synth.train_split(g.edge_index, 0.9, seed=0)
     n_tr = train_ei.shape[1]
@@ -537,8 +543,10 @@ def run_train(args):
         "value": K * edges / elapsed, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-        "data": "synthetic (seeded ML-25M-shaped graph, 90/5/5 directed split)",
-        "config": {"workload": f"C{3 if world == 1 else 4}_cluster_gcn_train", "parts": args.parts,
+        "data": ("synthetic (seeded ML-25M-sized graph with 1024 planted communities, 90/5/5 directed split)"
+                 if args.graph == "planted" else "synthetic (seeded ML-25M-shaped graph, 90/5/5 directed split)"),
+        "config": {"workload": f"C{3 if world == 1 else 4}_cluster_gcn_train" + ("_planted" if args.graph == "planted" else ""),
+                   "parts": args.parts, "mean_batch_edges": float(np.mean([b.edge_index.shape[1] for b in batches])),
                    "optimizer": ("torch Adam + clip_grad_norm_" if args.torch_adam else
                                  "lgcn RowLazyAdam (exact row-lazy Adam + clip, flushed each epoch)" if lazy else
                                  "lgcn FusedAdam (clip fused)"),

@@ -289,6 +289,17 @@ int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_
                            int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
                            const float* C2, float* c2buf, uint8_t* c2flag, int32_t* overflow,
                            const uint8_t* store_unless, lgcn_stream_t stream);
+/* The same per-row work as lgcn_range_scatter_add (flags, b-order sums, parked C2 sums, store or
+ * add) for LARGE B, where every range-scatter workgroup streaming all B keys would cost O(B^2):
+ * the keys arrive grouped by row in b order as rowptr[nrows+1] / perm[B] (= b) from
+ * lgcn_csr_build(keys, keys, B, nrows, ...), one stable radix sort. Bitwise the range scatter's
+ * result (same association) and it never overflows. Replaces, like lgcn_range_scatter_add, the
+ * negatives' share of the index_put_ accumulate in the backward of reference
+ * utils/train_test.py:128-134 (compute_embeddings' item_embedding gathers). */
+int lgcn_sorted_scatter_add(const int64_t* rowptr, const int32_t* perm, int64_t nrows, int64_t key_offset,
+                            const float* C, int32_t d, float* out_lo, float* out_hi, int64_t split, float mul,
+                            float div, const float* C2, float* c2buf, uint8_t* c2flag, const uint8_t* store_unless,
+                            lgcn_stream_t stream);
 int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, const float* c2buf,
                           const uint8_t* c2flag, int32_t d, float* out_lo, float* out_hi, int64_t split,
                           lgcn_stream_t stream);

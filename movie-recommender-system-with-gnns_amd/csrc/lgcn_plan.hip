@@ -31,14 +31,20 @@ __global__ void k_prep_keys(const int64_t* __restrict__ key, const int64_t* __re
     if (bad_local) atomicAdd(err, bad_local);
 }
 
-// rowptr from sorted keys: every row r in (keys[p-1], keys[p]] starts at slot p.
+// rowptr from sorted keys (all in [0, N)): rowptr[r] = the first slot whose key is >= r, by a
+// binary search per row — one thread per row, so runs of empty rows (touched-only batch plans,
+// segment plans built over max(N, M) rows) cost no serial loop.
 __global__ void k_rowptr_from_sorted(const int32_t* __restrict__ keys, int64_t E, int64_t N,
                                      int64_t* __restrict__ rowptr) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-    for (int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; p <= E; p += stride) {
-        const int64_t prev = (p == 0) ? -1 : keys[p - 1];
-        const int64_t cur = (p == E) ? N : keys[p];
-        for (int64_t r = prev + 1; r <= cur; ++r) rowptr[r] = p;
+    for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r <= N; r += stride) {
+        int64_t lo = 0, hi = E;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (keys[mid] < r) lo = mid + 1;
+            else hi = mid;
+        }
+        rowptr[r] = lo;
     }
 }
 
@@ -445,7 +451,7 @@ int lgcn_csr_build(const int64_t* key, const int64_t* other, int64_t E, int64_t 
                                                               key_bits(N), s),
                            "SortPairs(csr)"))
         return rc;
-    k_rowptr_from_sorted<<<grid_for(E + 1, kBlock, 8192), kBlock, 0, s>>>(k_out, E, N, rowptr);
+    k_rowptr_from_sorted<<<grid_for(N + 1, kBlock, 8192), kBlock, 0, s>>>(k_out, E, N, rowptr);
     if (int rc = check_launch("k_rowptr_from_sorted")) return rc;
     k_gather_col<<<grid_for(E, kBlock, 8192), kBlock, 0, s>>>(other, eid, E, N, col);
     return check_launch("k_gather_col");

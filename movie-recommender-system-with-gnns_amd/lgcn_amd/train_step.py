@@ -55,7 +55,10 @@ class _BatchState:
         # fixed (user, positive) gradient rows: load-balanced segment plans, built once per batch
         from .plan import segment_directions
 
-        self.small = 2 * B <= N  # segment plans index contributions as node ids (always true for real batches)
+        # fixed segment plans + range scatter (any batch whose 3B contribution ids fit int32; the
+        # plans are built over max(N, 2B) rows, so batches with 2B > N — structured graphs, where
+        # most edges stay intra-part — take this path too); else one sort of all keys per step
+        self.small = 3 * B < 2**31
         self.lazy = lazy and self.small
         if self.lazy:
             # row-lazy optimizer: only the batch's touched rows (and the negatives) are written
@@ -64,6 +67,19 @@ class _BatchState:
             self.touched_rows = torch.nonzero(self.plan.touched).squeeze(1).to(torch.int32).contiguous()
         elif self.small:
             self.fixed_dense, self.fixed_sparse = segment_directions(self.keys[:2 * B], N, chunk=32)
+        if self.small and B >= sorted_scatter_min_b():
+            # large B: the negatives are grouped by row with one stable radix sort per step
+            # (lgcn_csr_build over the B keys) and scattered row by row (lgcn_sorted_scatter_add)
+            self.neg_rowptr = torch.empty(I + 1, dtype=torch.int64, device=dev)
+            self.neg_col = torch.empty(B, dtype=torch.int32, device=dev)
+            self.neg_perm = torch.empty(B, dtype=torch.int32, device=dev)
+            self.neg_err = torch.zeros(1, dtype=torch.int64, device=dev)
+            lib_ = _ffi.load()
+            nb = _ffi._sz(0)
+            _ffi.check(lib_.lgcn_csr_workspace_size(B, I, nb), "lgcn_csr_workspace_size")
+            self.neg_ws = torch.empty(max(1, nb.value), dtype=torch.uint8, device=dev)
+        else:
+            self.neg_rowptr = None
         if self.small:
             self.c2buf = torch.empty((B, d), dtype=torch.float32, device=dev)
             self.c2flag = torch.empty(B, dtype=torch.uint8, device=dev)
@@ -81,6 +97,35 @@ class _BatchState:
         _ffi.check(lib.lgcn_csr_workspace_size(3 * B, N, nbytes), "lgcn_csr_workspace_size")
         self.ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=dev)
         self.plan.bwd  # build the transposed plan now (its build reads counts back once)
+
+
+def sorted_scatter_min_b() -> int:
+    """Batch size from which the negatives go through the sorted scatter instead of the range
+    scatter (whose key streaming grows as B^2): measured on the C3 graphs (B ~ 1e4: range
+    scatter ~10 us; B ~ 1.6e5: 627 us range vs sort + scatter). LGCN_SORTED_SCATTER_MIN_B overrides."""
+    import os
+
+    return int(os.environ.get("LGCN_SORTED_SCATTER_MIN_B", 49152))
+
+
+def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: float, store_unless, stream) -> None:
+    """dF rows of the step's negatives into the gradient tables, their reg rows parked per row
+    (first-occurrence slot, st.c2flag) for lgcn_flagged_rows_add after the backward."""
+    B = st.B
+    C, C2 = st.cf[2 * B:], st.cw[2 * B:]
+    if st.neg_rowptr is None:
+        _ffi.check(lib.lgcn_range_scatter_add(st.neg.data_ptr(), B, I, U, C.data_ptr(), d, gu.data_ptr(), gi.data_ptr(),
+                                              U, mul, div, C2.data_ptr(), st.c2buf.data_ptr(), st.c2flag.data_ptr(),
+                                              st.overflow.data_ptr(), _ffi.ptr(store_unless), stream),
+                   "lgcn_range_scatter_add")
+        return
+    _ffi.check(lib.lgcn_csr_build(st.neg.data_ptr(), st.neg.data_ptr(), B, I, st.neg_rowptr.data_ptr(),
+                                  st.neg_col.data_ptr(), st.neg_perm.data_ptr(), st.neg_err.data_ptr(),
+                                  st.neg_ws.data_ptr(), st.neg_ws.numel(), stream), "lgcn_csr_build(negatives)")
+    _ffi.check(lib.lgcn_sorted_scatter_add(st.neg_rowptr.data_ptr(), st.neg_perm.data_ptr(), I, U, C.data_ptr(), d,
+                                           gu.data_ptr(), gi.data_ptr(), U, mul, div, C2.data_ptr(),
+                                           st.c2buf.data_ptr(), st.c2flag.data_ptr(), _ffi.ptr(store_unless), stream),
+               "lgcn_sorted_scatter_add")
 
 
 class FusedTrainStep:
@@ -163,11 +208,7 @@ class FusedTrainStep:
                 spmm(st.fixed_dense, N, d, (st.cf, None, big), None, grads, None, _ffi.EPI_SCALE, div, mul,
                      stream=stream)
                 # negatives: dF rows into g now, their reg rows parked (per row, first-occurrence slot)
-                _ffi.check(lib.lgcn_range_scatter_add(st.neg.data_ptr(), B, I, U, st.cf[2 * B:].data_ptr(), d,
-                                                      gu.data_ptr(), gi.data_ptr(), U, mul, div,
-                                                      st.cw[2 * B:].data_ptr(), st.c2buf.data_ptr(),
-                                                      st.c2flag.data_ptr(), st.overflow.data_ptr(), None, stream),
-                           "lgcn_range_scatter_add")
+                scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, None, stream)
                 propagate_backward_seeded(gu, gi, st.plan, K)
                 spmm(st.fixed_sparse, N, d, (st.cw, None, big), None, grads, None, _ffi.EPI_ADD, stream=stream)
                 _ffi.check(lib.lgcn_flagged_rows_add(st.neg.data_ptr(), B, U, st.c2buf.data_ptr(),
@@ -230,11 +271,7 @@ class FusedTrainStep:
             spmm(st.fixed_touched, N, d, (st.cf, None, big), None, grads, None, _ffi.EPI_SCALE, div, mul,
                  stream=stream)
             # ... the negatives' rows added (stored where the row is outside the touched set)
-            _ffi.check(lib.lgcn_range_scatter_add(st.neg.data_ptr(), B, I, U, st.cf[2 * B:].data_ptr(), d,
-                                                  gu.data_ptr(), gi.data_ptr(), U, mul, div,
-                                                  st.cw[2 * B:].data_ptr(), st.c2buf.data_ptr(),
-                                                  st.c2flag.data_ptr(), st.overflow.data_ptr(),
-                                                  st.plan.touched.data_ptr(), stream), "lgcn_range_scatter_add")
+            scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream)
             propagate_backward_seeded(gu, gi, st.plan, K)
             spmm(st.fixed_sparse, N, d, (st.cw, None, big), None, grads, None, _ffi.EPI_ADD, stream=stream)
             _ffi.check(lib.lgcn_flagged_rows_add(st.neg.data_ptr(), B, U, st.c2buf.data_ptr(),

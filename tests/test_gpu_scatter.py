@@ -24,7 +24,7 @@ def _ref_scatter(keys, C, out, off, mul, div):
     return out, rows
 
 
-def _run(gpu, keys_np, nrows, off, d, N, mul, div, with_c2=True, seed=0):
+def _run(gpu, keys_np, nrows, off, d, N, mul, div, with_c2=True, seed=0, sorted_=False, store_unless=None):
     from lgcn_amd import _ffi
 
     lib = _ffi.load()
@@ -42,10 +42,27 @@ def _run(gpu, keys_np, nrows, off, d, N, mul, div, with_c2=True, seed=0):
     flag = torch.empty(max(B, 1), dtype=torch.uint8, device=gpu)
     ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
     s = _ffi.stream_of(gpu)
-    _ffi.check(lib.lgcn_range_scatter_add(keys.data_ptr(), B, nrows, off, Cg.data_ptr(), d, lo.data_ptr(),
-                                          hi.data_ptr(), split, mul, div,
-                                          C2g.data_ptr() if with_c2 else None, buf.data_ptr(), flag.data_ptr(),
-                                          ovf.data_ptr(), None, s), "lgcn_range_scatter_add")
+    su = None if store_unless is None else torch.from_numpy(store_unless).to(gpu)
+    if sorted_:  # one stable radix sort of the keys, then one lane group per row
+        rowptr = torch.empty(nrows + 1, dtype=torch.int64, device=gpu)
+        col = torch.empty(max(B, 1), dtype=torch.int32, device=gpu)
+        perm = torch.empty(max(B, 1), dtype=torch.int32, device=gpu)
+        err = torch.zeros(1, dtype=torch.int64, device=gpu)
+        nb = _ffi._sz(0)
+        _ffi.check(lib.lgcn_csr_workspace_size(B, nrows, nb), "ws")
+        ws = torch.empty(max(1, nb.value), dtype=torch.uint8, device=gpu)
+        _ffi.check(lib.lgcn_csr_build(keys.data_ptr(), keys.data_ptr(), B, nrows, rowptr.data_ptr(), col.data_ptr(),
+                                      perm.data_ptr(), err.data_ptr(), ws.data_ptr(), ws.numel(), s), "csr")
+        _ffi.check(lib.lgcn_sorted_scatter_add(rowptr.data_ptr(), perm.data_ptr(), nrows, off, Cg.data_ptr(), d,
+                                               lo.data_ptr(), hi.data_ptr(), split, mul, div,
+                                               C2g.data_ptr() if with_c2 else None, buf.data_ptr(), flag.data_ptr(),
+                                               _ffi.ptr(su), s), "lgcn_sorted_scatter_add")
+        assert int(err.item()) == 0
+    else:
+        _ffi.check(lib.lgcn_range_scatter_add(keys.data_ptr(), B, nrows, off, Cg.data_ptr(), d, lo.data_ptr(),
+                                              hi.data_ptr(), split, mul, div,
+                                              C2g.data_ptr() if with_c2 else None, buf.data_ptr(), flag.data_ptr(),
+                                              ovf.data_ptr(), _ffi.ptr(su), s), "lgcn_range_scatter_add")
     after1 = torch.cat([lo, hi]).cpu().numpy()
     if with_c2:
         _ffi.check(lib.lgcn_flagged_rows_add(keys.data_ptr(), B, off, buf.data_ptr(), flag.data_ptr(), d,
@@ -95,3 +112,38 @@ def test_range_scatter_overflow_is_reported(gpu):
     ref1, _ = _ref_scatter(keys, C, out0, 0, 1.0, 1.0)
     np.testing.assert_allclose(after1, ref1, rtol=1e-5, atol=1e-4)
     assert ovf == 1
+
+
+@pytest.mark.parametrize("B,nrows,d", [(1, 7, 64), (30000, 5000, 64), (162000, 59047, 128), (4000, 300000, 32),
+                                       (2000, 1000, 256), (9000, 4, 64)])
+def test_sorted_scatter_bitwise_range_scatter(gpu, B, nrows, d):
+    """lgcn_sorted_scatter_add (the large-B path) == the sequential restatement and, where the
+    range scatter stays in capacity, its output bitwise: the dF rows, the parked C2 sums, the
+    flags; with store_unless, rows it marks 0 are stored, not added to."""
+    rng = np.random.default_rng(B + d)
+    keys = rng.integers(0, nrows, B)
+    off = 5
+    N = off + nrows + 2
+    mul, div = float(np.float32(1 / 4)), 4.0
+    su = (rng.random(N) < 0.5).astype(np.uint8)
+    for store_unless in (None, su):
+        C, C2, out0, after1, after2, _, flag = _run(gpu, keys, nrows, off, d, N, mul, div, seed=1, sorted_=True,
+                                                     store_unless=store_unless)
+        base = out0.copy()
+        if store_unless is not None:
+            base[store_unless == 0] = 0.0  # stored rows: (0 + v) == v exactly
+        ref1, rows = _ref_scatter(keys, C, base, off, mul, div)
+        touched = np.zeros(N, bool)
+        touched[off + np.unique(keys)] = True
+        want1 = np.where(touched[:, None], ref1, out0)
+        np.testing.assert_array_equal(after1, want1)
+        ref2, _ = _ref_scatter(keys, C2, want1, off, 1.0, 1.0)
+        np.testing.assert_array_equal(after2, ref2)
+        firsts = sorted(bs[0] for bs in rows.values())
+        np.testing.assert_array_equal(np.nonzero(flag)[0], firsts)
+        if B <= 4096 * 8 and store_unless is None and len(np.unique(keys)) > 4:
+            _, _, _, r1, r2, ovf, rflag = _run(gpu, keys, nrows, off, d, N, mul, div, seed=1)
+            if ovf == 0:
+                np.testing.assert_array_equal(after1, r1)
+                np.testing.assert_array_equal(after2, r2)
+                np.testing.assert_array_equal(flag, rflag)

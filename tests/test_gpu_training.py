@@ -262,8 +262,9 @@ def test_row_lazy_adam_matches_dense_fused_adam(gpu, clip):
             assert (a.detach() - b).abs().max().item() <= 1e-6 * a.abs().max().item()
 
 
-@pytest.mark.parametrize("use_graphs,clip", [(False, float("inf")), (True, float("inf")), (False, 1.0)])
-def test_lazy_train_step_matches_dense_step(gpu, use_graphs, clip):
+@pytest.mark.parametrize("use_graphs,clip,whole", [(False, float("inf"), False), (True, float("inf"), False),
+                                                   (False, 1.0, False), (True, float("inf"), True)])
+def test_lazy_train_step_matches_dense_step(gpu, use_graphs, clip, whole):
     """FusedTrainStep(lazy=True) + RowLazyAdam == FusedTrainStep + dense capturable FusedAdam on
     the same Cluster-GCN batches and negatives. Without clipping (max_norm = inf, coefficient
     exactly 1): bitwise, every loss and every parameter (eager and hipGraph-replayed). With clip_grad_norm_(1): the two norms sum the same
@@ -281,6 +282,9 @@ def test_lazy_train_step_matches_dense_step(gpu, use_graphs, clip):
     part = C.partition_nodes(ei, U + I, 8)
     batches = [_Batch(torch.from_numpy(x).to(gpu)) for x in C.intra_part_edges(ei, part, 8)]
     assert all(2 * int((b.edge_index[0] < U).sum()) <= U + I for b in batches)
+    if whole:  # one batch = the whole graph: 2B > N (big intra-part batches of structured graphs)
+        batches = [_Batch(torch.from_numpy(ei).to(gpu))] * 8
+        assert 2 * int((batches[0].edge_index[0] < U).sum()) > U + I
     res = []
     for lazy in (False, True):
         torch.manual_seed(0)
@@ -380,3 +384,41 @@ def test_recall_parity_c1_size(gpu, cpu_negatives):
         print(f"C1 Recall@{k}: hip {out['hip'][k]:.5f} ref {out['ref'][k]:.5f} |diff| {d:.5f} "
               f"(rel {d / max(out['ref'][k], 1e-12):.2e}; bar 0.002)")
         assert d <= 0.002, (k, out)
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+def test_sorted_negatives_path_bitwise_range_path(gpu, monkeypatch, lazy):
+    """The large-B negatives path (one radix sort + lgcn_sorted_scatter_add, taken from
+    LGCN_SORTED_SCATTER_MIN_B triplets) gives bitwise the range-scatter path's losses and
+    parameters over 12 hipGraph-replayed steps (dense FusedAdam and row-lazy Adam)."""
+    from lgcn_amd import cluster as C
+    from lgcn_amd.optim import FusedAdam, RowLazyAdam
+    from lgcn_amd.train_step import FusedTrainStep
+    from models.light_gcn import LightGCN
+
+    import graphs
+
+    U, I, ei = graphs.subsampled(U=2000, I=1000, pairs=8000, seed=4)
+    part = C.partition_nodes(ei, U + I, 4)
+    batches = [_Batch(torch.from_numpy(x).to(gpu)) for x in C.intra_part_edges(ei, part, 4)]
+    batches.append(_Batch(torch.from_numpy(ei).to(gpu)))  # one 2B > N batch
+    res = []
+    for min_b in ("1000000000", "1"):
+        monkeypatch.setenv("LGCN_SORTED_SCATTER_MIN_B", min_b)
+        torch.manual_seed(0)
+        m = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
+        if lazy:
+            opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-2, max_grad_norm=1.0)
+        else:
+            opt = FusedAdam(m.parameters(), lr=1e-2, max_grad_norm=1.0, capturable=True)
+        step = FusedTrainStep(m, opt, graphs=True, lazy=lazy)
+        losses = []
+        for i in range(12):
+            torch.cuda.manual_seed(50 + i)
+            losses.append(step.step(batches[i % len(batches)]).item())
+        step.sync()
+        st = step.state(batches[-1].edge_index)
+        assert (st.neg_rowptr is not None) == (min_b == "1")
+        res.append((losses, m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
