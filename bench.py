@@ -7,10 +7,11 @@ models/light_gcn.py:28-40) with the plan (CSR + gcn_norm + schedule) already bui
 embedding tables resident in HBM. value = K * E / wall time per step: ONE graph at every N.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
-GPU, strong scaling. C2 is row-sharded (lgcn_amd.sharded): each rank propagates its own
-edge-balanced destination rows of the same graph, and each layer's two output blocks (user rows,
-item rows) are all-gathered over RCCL on a side stream while the other half-layer computes;
-the result is bitwise the 1-GPU result. C5 (--config c5) is feature-sharded: d/N columns per
+GPU, strong scaling. C2 is sharded over an R x F grid (lgcn_amd.sharded): F column groups (each
+propagates d/F columns, no exchange between them) times R row groups (each rank propagates its
+own edge-balanced destination rows of the same graph, and each layer's two output blocks (user
+rows, item rows) are all-gathered over RCCL within the column group on a side stream while the
+other half-layer computes); the result is bitwise the 1-GPU result. C5 (--config c5) is feature-sharded: d/N columns per
 rank, no collective. The barrier and the max-over-ranks time go over RCCL.
 
 Also reported (one JSON line on rank 0):
@@ -219,6 +220,9 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="graph scale vs ML-25M (1.0 = C2)")
     ap.add_argument("--chunk", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", default=None,
+                    help="c2, N > 1: RxF grid (R row groups x F column groups, R*F = N); default "
+                         "lgcn_amd.sharded.grid_shape (two column groups when N is even and d/2 >= 32)")
     ap.add_argument("--workload", choices=["propagate", "train"], default="propagate",
                     help="propagate: C2 headline (default); train: C3/C4 Cluster-GCN training steps")
     ap.add_argument("--parts", type=int, default=1024, help="train: Cluster-GCN parts")
@@ -295,18 +299,26 @@ def main():
     t0 = time.perf_counter()
     exchange = None
     if sharded:
-        from lgcn_amd.sharded import BlockExchange, RowShards, ShardedPlan, propagate_forward_sharded
+        from lgcn_amd.sharded import BlockExchange, RowShards, ShardedPlan, ShardGrid, propagate_forward_sharded
 
-        shards = RowShards.build(np.bincount(graph.edge_index[1], minlength=N), U, world)
-        splan = ShardedPlan(ei, shards, rank, d, chunk)
-        x0p = shards.to_padded(user_w, item_w)
-        exchange = BlockExchange(shards, rank)
+        R, F = (int(v) for v in args.shard.split("x")) if args.shard else (None, None)
+        grid = ShardGrid.build(world, rank, d_full, R, F)
+        c0, c1 = grid.cols
+        d = c1 - c0
+        g_r = grid.row_group
+        shards = RowShards.build(np.bincount(graph.edge_index[1], minlength=N), U, grid.R)
+        splan = ShardedPlan(ei, shards, g_r, d, chunk, slice_d=d_full)
+        x0p = shards.to_padded(user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous())
+        del user_w, item_w
+        group = grid.exchange_group(dist)  # collective: every rank creates the column groups
+        exchange = BlockExchange(shards, g_r, group) if grid.R > 1 else None
         scheds = [h.direction for h in splan.halves]
         torch.cuda.synchronize()
-        ua, ub_ = shards.user_rows(rank)
-        ia, ib_ = shards.item_rows(rank)
-        log(f"[rank {rank}] row shard: users {ub_ - ua} (of {U}), items {ib_ - ia} (of {I}), padded N {shards.NP}; "
-            f"{'sliced' if splan.sliced else 'plain'} halves, {time.perf_counter() - t0:.2f} s")
+        ua, ub_ = shards.user_rows(g_r)
+        ia, ib_ = shards.item_rows(g_r)
+        log(f"[rank {rank}] grid {grid.R}x{grid.F}: row group {g_r} (users {ub_ - ua} of {U}, items {ib_ - ia} of "
+            f"{I}), columns [{c0}, {c1}); padded N {shards.NP}; {'sliced' if splan.sliced else 'plain'} halves, "
+            f"{time.perf_counter() - t0:.2f} s")
 
         def step():
             return propagate_forward_sharded(x0p, splan, K, exchange)
@@ -353,7 +365,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0].item()), float(t[1].item())
 
-    # one graph in every configuration: C2 row-sharded / C5 column-sharded over the ranks
+    # one graph in every configuration: C2 on an R x F grid / C5 column-sharded over the ranks
     value = K * E * args.steps / elapsed
     # bytes of one middle layer's item pass (this rank's rows), spread over its launches
     comp_layer, launches, e_mine, n_mine = 0, 0, 0, 0
@@ -366,9 +378,9 @@ def main():
     if c5:
         workload = f"C5_synthetic_10Mx1M_5e8_K{K}_d{d_full}" + ("" if args.scale == 1.0 else f"_scale{args.scale}")
     else:
-        workload = f"C2_ml25m_shaped_K{K}_d{d}" + ("" if args.scale == 1.0 else f"_scale{args.scale}")
+        workload = f"C2_ml25m_shaped_K{K}_d{d_full}" + ("" if args.scale == 1.0 else f"_scale{args.scale}")
         if sharded:
-            workload += f"_rowshard{world}"
+            workload += f"_grid{grid.R}x{grid.F}"
     if c5 and world > 1:
         workload_pmc = None
     else:
@@ -396,10 +408,12 @@ def main():
                    "chunk": chunk, "graphs": 1,
                    "parallelism": (f"feature-sharded over {world} GPU(s): {d} columns each, full plan per rank, "
                                    "no collective") if c5 else
-                                  (f"row-sharded over {world} GPUs: edge-balanced destination row ranges, the whole "
-                                   f"table on every rank, 2 block all_gathers (RCCL) per exchanged layer, each "
-                                   f"overlapped with the other half-layer; bitwise the 1-GPU result" if sharded else
-                                   "single GPU")},
+                                  (f"{grid.R} row groups x {grid.F} column groups over {world} GPUs: each rank "
+                                   f"propagates {d} of {d_full} columns of one edge-balanced destination row range "
+                                   f"(whole graph and whole column share of the table on every rank); ranks of a column "
+                                   f"group all_gather (RCCL) each exchanged layer's two row blocks, each overlapped "
+                                   f"with the other half-layer; column groups exchange nothing; bitwise the 1-GPU "
+                                   f"result" if sharded else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "basis": basis,
                      "kernel": (f"k_spmm_vec<{kernel_lpr(d)},sliced> (lgcn_spmm_run_slices, {launches} source-slice "

@@ -187,33 +187,48 @@ __device__ __forceinline__ void sum_item(const SpmmArgs& a, const lgcn_item_t it
     }
 }
 
-// Block-split launches (lgcn_spmm_blocksplit): workgroup s < n_splits sums split row s whole.
-// Group g sums chunks g, g+GPB, ... (each from 0, in CSR order — the partial the item pass would
-// have written) into its running sum in that order, and the GPB sums are added in group order
-// through LDS: the association of item pass + k_combine_vec, so bitwise the same result,
-// without the partials' round trip or the second launch.
+// Split rows (chunked hubs) are summed with ONE association at every width: partial/chunk c goes
+// to running sum v = c % kVSums (in c order), then the kVSums sums are added in v order. Lane
+// group g of a workgroup owns sums g, g + GPB, ... (GPB = groups per block: 64 at d=16, 16 at
+// d=64, 4 at d >= 256), so a row's result does not depend on d — a column share of a row (the
+// column-split sharded forward, lgcn_amd.sharded) is bitwise that share of the full-width row.
+constexpr int kVSums = 16;
+
+// Block-split launches (lgcn_spmm_blocksplit): workgroup s < n_splits sums split row s whole:
+// each chunk (from 0, in CSR order — the partial the item pass would have written) into its
+// running sum, then the sums in order through LDS: the association of item pass + k_combine_vec,
+// so bitwise the same result, without the partials' round trip or the second launch.
 template <int LPR, int NV, int UNROLL, int TAIL>
 __device__ __forceinline__ void split_row_block(const SpmmArgs& a, int64_t s, int g, int l) {
     constexpr int GPB = kBlock / LPR;
-    __shared__ float4 lds[GPB][LPR * NV];
+    constexpr int VPG = (kVSums + GPB - 1) / GPB;
+    __shared__ float4 lds[kVSums][LPR * NV];
     const lgcn_split_t sp = a.splits[s];
-    float4 acc[NV];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int c = g; c < sp.pcnt; c += GPB) {
-        float4 part[NV];
+    for (int j = 0; j < VPG; ++j) {
+        const int v = g + j * GPB;
+        if (v >= kVSums) break;
+        float4 acc[NV];
 #pragma unroll
-        for (int k = 0; k < NV; ++k) part[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        sum_item<LPR, NV, UNROLL, TAIL>(a, a.chunks[int64_t(sp.pbeg) + c], l, part);
+        for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int c = v; c < sp.pcnt; c += kVSums) {
+            float4 part[NV];
 #pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], part[k]);
+            for (int k = 0; k < NV; ++k) part[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            sum_item<LPR, NV, UNROLL, TAIL>(a, a.chunks[int64_t(sp.pbeg) + c], l, part);
+#pragma unroll
+            for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], part[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < NV; ++k) lds[v][l + k * LPR] = acc[k];
     }
-#pragma unroll
-    for (int k = 0; k < NV; ++k) lds[g][l + k * LPR] = acc[k];
     __syncthreads();
     if (g != 0) return;
-    const int ng = sp.pcnt < GPB ? sp.pcnt : GPB;
-    for (int h = 1; h < ng; ++h)
+    float4 acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = lds[0][l + k * LPR];
+    const int nv = sp.pcnt < kVSums ? sp.pcnt : kVSums;
+    for (int h = 1; h < nv; ++h)
 #pragma unroll
         for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], lds[h][l + k * LPR]);
     finish_row_vec<LPR, NV>(a, sp.row, l, acc);
@@ -267,14 +282,16 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
     finish_row_vec<LPR, NV>(a, it.dst, l, acc);
 }
 
-// Split rows: one workgroup per split row. Group g (of GPB) sums partials g, g+GPB, g+2*GPB, ...
-// with UNROLL loads in flight; the GPB group sums are then added in group order through LDS.
-// The association is fixed by the code, so results are deterministic run to run.
+// Split rows: one workgroup per split row. Running sum v (of kVSums, owned by lane group v % GPB)
+// adds partials v, v + kVSums, ... with UNROLL loads in flight; the kVSums sums are then added in
+// v order through LDS. The association is fixed by the code and the same at every width, so
+// results are deterministic run to run and a column share is bitwise the full row's share.
 template <int LPR, int NV>
 __global__ __launch_bounds__(kBlock) void k_combine_vec(SpmmArgs a) {
     constexpr int GPB = kBlock / LPR;
+    constexpr int VPG = (kVSums + GPB - 1) / GPB;
     constexpr int UNROLL = 4;
-    __shared__ float4 lds[GPB][LPR * NV];
+    __shared__ float4 lds[kVSums][LPR * NV];
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
     const int64_t s = blockIdx.x;
@@ -282,30 +299,38 @@ __global__ __launch_bounds__(kBlock) void k_combine_vec(SpmmArgs a) {
     const lgcn_split_t sp = a.splits[s];
     const int64_t d4 = int64_t(LPR) * NV;
     const float4* p = reinterpret_cast<const float4*>(a.partial) + int64_t(sp.pbeg) * d4;
-    float4 acc[NV];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    int c = g;
-    for (; c + (UNROLL - 1) * GPB < sp.pcnt; c += UNROLL * GPB) {
-        float4 t[UNROLL][NV];
+    for (int j = 0; j < VPG; ++j) {
+        const int v = g + j * GPB;
+        if (v >= kVSums) break;
+        float4 acc[NV];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u)
+        for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        int c = v;
+        for (; c + (UNROLL - 1) * kVSums < sp.pcnt; c += UNROLL * kVSums) {
+            float4 t[UNROLL][NV];
 #pragma unroll
-            for (int k = 0; k < NV; ++k) t[u][k] = p[int64_t(c + u * GPB) * d4 + l + k * LPR];
+            for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u)
+                for (int k = 0; k < NV; ++k) t[u][k] = p[int64_t(c + u * kVSums) * d4 + l + k * LPR];
 #pragma unroll
-            for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], t[u][k]);
+            for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+                for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], t[u][k]);
+        }
+        for (; c < sp.pcnt; c += kVSums)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], p[int64_t(c) * d4 + l + k * LPR]);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) lds[v][l + k * LPR] = acc[k];
     }
-    for (; c < sp.pcnt; c += GPB)
-#pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], p[int64_t(c) * d4 + l + k * LPR]);
-#pragma unroll
-    for (int k = 0; k < NV; ++k) lds[g][l + k * LPR] = acc[k];
     __syncthreads();
     if (g != 0) return;
-    const int ng = sp.pcnt < GPB ? sp.pcnt : GPB;
-    for (int h = 1; h < ng; ++h)
+    float4 acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = lds[0][l + k * LPR];
+    const int nv = sp.pcnt < kVSums ? sp.pcnt : kVSums;
+    for (int h = 1; h < nv; ++h)
 #pragma unroll
         for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], lds[h][l + k * LPR]);
     finish_row_vec<LPR, NV>(a, sp.row, l, acc);

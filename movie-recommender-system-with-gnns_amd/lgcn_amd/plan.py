@@ -23,6 +23,15 @@ import torch
 from . import _ffi
 
 DEFAULT_CHUNK = 256
+# hub chunk of the source-sliced schedule: a chunk is one lane group's sequential chain (one L2
+# latency per 8 edges), and every slice launch waits for its longest chain; 128 measured 2 %
+# faster than 256 on C2 and 1.4-1.6x faster on the small per-rank schedules of the sharded forward
+# (profiles/r02k_shard/)
+SLICED_CHUNK = 128
+
+
+def sliced_chunk(chunk: int) -> int:
+    return min(int(chunk), SLICED_CHUNK)
 # batch plans (touched-only, segment) use the one-launch block-split schedule; LGCN_BLOCKSPLIT=0
 # keeps them on item pass + combine (A/B knob)
 BLOCK_SPLIT = os.environ.get("LGCN_BLOCKSPLIT", "1") != "0"
@@ -233,7 +242,7 @@ class PropagationPlan:
             # (C2: 112 edges per row; a 5 % validation edge set, ~6, is faster unsliced)
             forced = os.environ.get("LGCN_SLICE_MB") is not None
             if forced or self.num_edges >= 8 * (len(bounds) - 1) * self.num_nodes:
-                out = build_sliced(direction, self.num_nodes, bounds, direction.chunk) or direction
+                out = build_sliced(direction, self.num_nodes, bounds, sliced_chunk(direction.chunk)) or direction
         self._sched[key] = out
         return out
 

@@ -1,5 +1,7 @@
-"""Row-sharded full-graph propagation over W GPUs (BASELINE.json's headline
-"edges propagated/sec (K=3, d=64) at 1/2/4/8 GPUs" on configs[1]).
+"""Sharded full-graph propagation over W GPUs (SURVEY.md §8e (i)+(ii); BASELINE.json's headline
+"edges propagated/sec (K=3, d=64) at 1/2/4/8 GPUs" on configs[1]): an R x F grid of ranks,
+R row groups (below) times F column groups (``ShardGrid``: each column group propagates its
+d / F columns of every row it owns, with no exchange between column groups).
 
 One graph, one K-layer LightGCN forward (reference models/light_gcn.py:28-40), split over W
 ranks by DESTINATION rows; the total work is fixed (strong scaling):
@@ -12,8 +14,12 @@ ranks by DESTINATION rows; the total work is fixed (strong scaling):
   so one layer's rows of every rank land with one ``all_gather_into_tensor`` per block (equal
   chunks, no copy). Node ids are remapped by ``RowShards.padmap``, which is strictly increasing:
   every row keeps its neighbours in the same order, so its sum is the same chain of additions as
-  on one GPU. The source-slice bounds of the one-GPU schedule are mapped the same way, so hub
-  rows are cut into the same chunks: the sharded result is BITWISE the one-GPU result.
+  on one GPU. Schedules: with one row group (R = 1, columns split only) a rank runs the one-GPU
+  schedule itself (the source-slice bounds of the full width, mapped the same way), so hub rows
+  are cut into the same chunks and the result is BITWISE the one-GPU result. With R > 1 a rank
+  runs the plain item schedule (one launch per half-layer, ``rank_chunk``): bitwise the one-GPU
+  plain schedule at that chunk, and within 1e-5 of the default (sliced) one, whose hub rows are
+  chunked at slice boundaries too.
 * Exchange overlapped with compute (bipartite graphs: every edge joins a user and an item).
   User rows gather only item rows and item rows only user rows, so a layer splits into two
   halves that share no row: A = the user-source slices (writes the item rows), B = the
@@ -138,6 +144,75 @@ class RowShards:
         return xp[torch.from_numpy(self.padmap()).to(xp.device)]
 
 
+def rank_chunk(chunk: int, R: int) -> int:
+    """Hub chunk of a rank's schedule: the one-GPU chunk with one row group (same schedule as one
+    GPU, so bitwise its result); with R > 1 the plain schedule at min(chunk, SLICED_CHUNK) (a
+    shorter longest chain per launch; per-rank K=3 step at 8x1: 0.253 ms at 256, 0.246 at 128)."""
+    from .plan import SLICED_CHUNK
+
+    return int(chunk) if R == 1 else min(int(chunk), SLICED_CHUNK)
+
+
+MIN_COLS = 32  # a column share narrower than 128 B rows stops cutting gather requests per edge
+
+
+def grid_shape(world: int, d: int) -> tuple[int, int]:
+    """(R row groups, F column groups), R * F = world. The item pass is bound by gather requests
+    per edge, not bytes: halving a 256-B row to 128 B halves the requests (C2, one GPU: 1.72 ->
+    0.94 ms per K=3 step at d = 64 -> 32, plain schedule), narrower rows do not (d = 16: 1.28 ms).
+    Splitting columns needs no exchange, splitting rows needs an all_gather per layer, so two
+    column groups are used whenever the world is even and d / 2 >= MIN_COLS; the rest are rows."""
+    if world >= 2 and world % 2 == 0 and d % 2 == 0 and d // 2 >= MIN_COLS and (d // 2) % 4 == 0:
+        return world // 2, 2
+    return world, 1
+
+
+@dataclasses.dataclass
+class ShardGrid:
+    """Rank r of an R x F grid: row group r // F (RowShards rank), column group r % F (columns
+    [c0, c1) of the tables). Ranks of one column group exchange their rows (an all_gather over R
+    ranks); column groups never exchange anything."""
+
+    world: int
+    rank: int
+    R: int
+    F: int
+    d: int
+
+    @classmethod
+    def build(cls, world: int, rank: int, d: int, R: int | None = None, F: int | None = None) -> "ShardGrid":
+        if R is None or F is None:
+            R, F = grid_shape(world, d)
+        if R * F != world or d % F or (d // F) % 4:
+            raise ValueError(f"bad shard grid {R}x{F} for world {world}, d {d}")
+        return cls(world, rank, R, F, d)
+
+    @property
+    def row_group(self) -> int:
+        return self.rank // self.F
+
+    @property
+    def col_group(self) -> int:
+        return self.rank % self.F
+
+    @property
+    def cols(self) -> tuple[int, int]:
+        w = self.d // self.F
+        return self.col_group * w, (self.col_group + 1) * w
+
+    def exchange_group(self, dist):
+        """The process group of this rank's column group (None = the default group when F = 1).
+        Every rank must call this (new_group is collective over the world)."""
+        if self.F == 1:
+            return None
+        mine = None
+        for c in range(self.F):
+            g = dist.new_group(ranks=[c + self.F * i for i in range(self.R)])
+            if c == self.col_group:
+                mine = g
+        return mine
+
+
 @dataclasses.dataclass
 class Half:
     """One piece of a layer: the schedule of the rows it writes and the blocks it reads/writes."""
@@ -152,15 +227,19 @@ class ShardedPlan:
     """Rank `rank`'s propagation plan of a row-sharded graph: the whole (padded) CSR with gcn_norm
     weights from the whole graph's degrees, and the schedules of its own rows, per half."""
 
-    def __init__(self, edge_index: torch.Tensor, shards: RowShards, rank: int, d: int, chunk: int | None = None):
-        from .plan import DEFAULT_CHUNK, CsrDirection, _build_direction, _schedule, slice_bytes_for
+    def __init__(self, edge_index: torch.Tensor, shards: RowShards, rank: int, d: int, chunk: int | None = None,
+                 slice_d: int | None = None):
+        """d: the width this rank propagates (its column share); slice_d: the width whose one-GPU
+        slicing decision and bounds are kept (the full d when columns are split too), so every
+        row keeps the one-GPU segments and hub chunks."""
+        from .plan import DEFAULT_CHUNK, CsrDirection, _build_direction, _schedule, slice_bytes_for, sliced_chunk
         from .sliced import build_sliced, slice_bounds
 
         _ffi.require_device(edge_index, "ShardedPlan")
         if edge_index.dim() != 2 or edge_index.shape[0] != 2 or edge_index.dtype != torch.int64:
             raise ValueError("edge_index must be int64 [2, E]")
         self.shards, self.rank, self.d = shards, int(rank), int(d)
-        self.chunk = int(chunk or DEFAULT_CHUNK)
+        self.chunk = rank_chunk(int(chunk or DEFAULT_CHUNK), shards.W)
         dev = edge_index.device
         self.device = dev
         N, U, NP, side = shards.N, shards.U, shards.NP, shards.side
@@ -185,15 +264,22 @@ class ShardedPlan:
             pieces = [("ui", "ui", owned)]
         # the one-GPU plan's slicing decision and bounds (lgcn_amd.plan.PropagationPlan.schedule),
         # mapped to padded ids: the same segments, the same hub chunks
-        sb = slice_bytes_for(N, d)
-        bounds = slice_bounds(N, U, d, sb) if (sb and E) else None
+        sd_ = int(slice_d or d)
+        sb = slice_bytes_for(N, sd_)
+        bounds = slice_bounds(N, U, sd_, sb) if (sb and E) else None
         if bounds is not None and not (E >= 8 * (len(bounds) - 1) * N or _slice_forced()):
             bounds = None
         self.halves: list[Half] = []
+        # R > 1 (a rank holds a 1/R share of the rows): the plain item schedule, one launch per
+        # half-layer, hub chunks of rank_chunk rows — a slice launch's fixed cost (its longest
+        # chunk chain, ~10-25 us) outweighs the L2 locality it buys at that size
+        # (profiles/r02k_shard/: per-rank K=3 step at 8x1 0.59 ms sliced, 0.25 ms plain)
+        if shards.W > 1:
+            bounds = None
         for reads, writes, mask in pieces:
             direction = None
             if bounds is not None:
-                direction = build_sliced(self.fwd, NP, shards.pad_bounds(bounds), self.chunk, mask)
+                direction = build_sliced(self.fwd, NP, shards.pad_bounds(bounds), sliced_chunk(self.chunk), mask)
             if direction is None:
                 f = self.fwd
                 direction = CsrDirection(f.rowptr, f.col, f.eid, f.val,
@@ -201,7 +287,9 @@ class ShardedPlan:
             partial = (torch.empty((direction.n_partials, d), dtype=torch.float32, device=dev)
                        if direction.n_partials else None)
             self.halves.append(Half(direction, reads, writes, partial))
+        # sliced: the running-sum buffers are needed (per-slice launches)
         self.sliced = bounds is not None and all(hasattr(h.direction, "launches") for h in self.halves)
+        self.slice_bounds = bounds
 
     @property
     def NP(self) -> int:
@@ -231,6 +319,8 @@ class BlockExchange:
     gloo (tests, rehearsal): the same collective through host memory, synchronously."""
 
     def __init__(self, shards: RowShards, rank: int, group=None):
+        """rank: this rank's index among the ranks that share its columns (its RowShards rank);
+        group: their process group (None = the default group)."""
         import torch.distributed as dist
 
         self.dist = dist

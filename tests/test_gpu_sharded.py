@@ -35,36 +35,55 @@ def _graph(kind):
     return graphs.subsampled(U=400, I=300, pairs=6000, seed=2)
 
 
-def _reference(dev, case):
-    """One-GPU forward with the same plan settings."""
+def _reference(dev, case, R=1):
+    """One-GPU forward with the schedule a rank of R row groups runs: the default one (R = 1), or
+    the plain schedule at lgcn_amd.sharded.rank_chunk (R > 1)."""
     from lgcn_amd import propagate_forward
     from lgcn_amd.plan import PropagationPlan
+    from lgcn_amd.sharded import rank_chunk
 
     kind, K, d, chunk, slice_mb = CASES[case]
     U, I, ei = _graph(kind)
     import graphs
 
     uw, iw = graphs.embeddings(U, I, d, seed=K + d)
-    plan = PropagationPlan(torch.from_numpy(ei).to(dev), U + I, chunk, side_split=U)
-    out = propagate_forward(torch.from_numpy(uw).to(dev), torch.from_numpy(iw).to(dev), plan, K)
-    return U, I, ei, uw, iw, out.cpu().numpy(), plan.schedule("fwd", d)
+    saved = os.environ.get("LGCN_SLICE_MB")
+    if R > 1:
+        os.environ["LGCN_SLICE_MB"] = "0"
+    try:
+        plan = PropagationPlan(torch.from_numpy(ei).to(dev), U + I, rank_chunk(chunk, R), side_split=U)
+        out = propagate_forward(torch.from_numpy(uw).to(dev), torch.from_numpy(iw).to(dev), plan, K)
+        sched = plan.schedule("fwd", d)
+    finally:
+        if saved is None:
+            os.environ.pop("LGCN_SLICE_MB", None)
+        else:
+            os.environ["LGCN_SLICE_MB"] = saved
+    return U, I, ei, uw, iw, out.cpu().numpy(), sched
 
 
-def _sharded(dev, case, world, rank):
-    from lgcn_amd.sharded import BlockExchange, RowShards, ShardedPlan, propagate_forward_sharded
+def _sharded(dev, case, world, rank, F=1):
+    from lgcn_amd.sharded import BlockExchange, RowShards, ShardedPlan, ShardGrid, propagate_forward_sharded
 
     kind, K, d, chunk, slice_mb = CASES[case]
     U, I, ei = _graph(kind)
     import graphs
 
     uw, iw = graphs.embeddings(U, I, d, seed=K + d)
-    shards = RowShards.build(np.bincount(ei[1], minlength=U + I), U, world)
-    splan = ShardedPlan(torch.from_numpy(ei).to(dev), shards, rank, d, chunk)
-    x0p = shards.to_padded(torch.from_numpy(uw).to(dev), torch.from_numpy(iw).to(dev))
-    ex = BlockExchange(shards, rank) if world > 1 else None
+    grid = ShardGrid.build(world, rank, d, world // F, F)
+    c0, c1 = grid.cols
+    g_r = grid.row_group
+    shards = RowShards.build(np.bincount(ei[1], minlength=U + I), U, grid.R)
+    # the column share keeps the full width's slicing, so rows keep the one-GPU segments
+    splan = ShardedPlan(torch.from_numpy(ei).to(dev), shards, g_r, c1 - c0, chunk, slice_d=d)
+    x0p = shards.to_padded(torch.from_numpy(uw[:, c0:c1].copy()).to(dev), torch.from_numpy(iw[:, c0:c1].copy()).to(dev))
+    import torch.distributed as dist
+
+    group = grid.exchange_group(dist) if world > 1 else None
+    ex = BlockExchange(shards, g_r, group) if grid.R > 1 else None
     out = propagate_forward_sharded(x0p, splan, K, ex).cpu().numpy()
-    a, b = shards.user_rows(rank)
-    c, e = shards.item_rows(rank)
+    a, b = shards.user_rows(g_r)
+    c, e = shards.item_rows(g_r)
     return shards, splan, out[a:b], out[c:e]
 
 
@@ -88,7 +107,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, case, out_dir):
+def _worker(rank, world, port, case, out_dir, F=1):
     import sys
 
     from conftest import PKG, ROOT
@@ -103,27 +122,40 @@ def _worker(rank, world, port, case, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    shards, splan, ou, oi = _sharded(dev, case, world, rank)
-    np.save(os.path.join(out_dir, f"u{rank}.npy"), ou)
-    np.save(os.path.join(out_dir, f"i{rank}.npy"), oi)
+    shards, splan, ou, oi = _sharded(dev, case, world, rank, F)
+    g_r, c_g = rank // F, rank % F
+    np.save(os.path.join(out_dir, f"u{g_r}_{c_g}.npy"), ou)
+    np.save(os.path.join(out_dir, f"i{g_r}_{c_g}.npy"), oi)
     np.save(os.path.join(out_dir, f"n{rank}.npy"),
             np.array([sum(getattr(h.direction, "n_splits", 0) for h in splan.halves), int(splan.sliced)]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", list(CASES))
-def test_sharded_two_ranks_bitwise(gpu, monkeypatch, tmp_path, case):
+@pytest.mark.parametrize("case,world,F", [(c, 2, 1) for c in CASES] + [("ml25m5_sliced", 2, 2), ("hub_sliced", 2, 2),
+                                                                     ("ml25m5_sliced", 4, 2), ("sub_K2_d128", 4, 2)])
+def test_sharded_ranks_bitwise(gpu, monkeypatch, tmp_path, case, world, F):
+    """world / F row groups x F column groups (gloo, every rank on the one GPU): the assembled
+    output is bitwise the one-GPU forward at the full width with the schedule the ranks run
+    (lgcn_amd.sharded.rank_chunk); with R > 1 also within 1e-5 per row of the default one."""
     slice_mb = CASES[case][4]
     if slice_mb:
         monkeypatch.setenv("LGCN_SLICE_MB", slice_mb)
-    U, I, ei, uw, iw, ref, sched = _reference(gpu, case)
+    R = world // F
+    U, I, ei, uw, iw, ref, sched = _reference(gpu, case, R)
     torch.cuda.synchronize()
-    mp.spawn(_worker, args=(2, _free_port(), case, str(tmp_path)), nprocs=2, join=True)
-    got_u = np.concatenate([np.load(tmp_path / f"u{r}.npy") for r in range(2)])
-    got_i = np.concatenate([np.load(tmp_path / f"i{r}.npy") for r in range(2)])
+    mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path), F), nprocs=world, join=True)
+    got_u = np.concatenate([np.concatenate([np.load(tmp_path / f"u{r}_{c}.npy") for c in range(F)], axis=1)
+                            for r in range(R)])
+    got_i = np.concatenate([np.concatenate([np.load(tmp_path / f"i{r}_{c}.npy") for c in range(F)], axis=1)
+                            for r in range(R)])
     assert np.array_equal(got_u, ref[:U]) and np.array_equal(got_i, ref[U:])
-    meta = [np.load(tmp_path / f"n{r}.npy") for r in range(2)]
+    if R > 1:
+        from parity import assert_rows_close
+
+        default = _reference(gpu, case, 1)[5]
+        assert_rows_close(np.concatenate([got_u, got_i]), default, what="sharded vs default schedule")
+    meta = [np.load(tmp_path / f"n{r}.npy") for r in range(world)]
     assert all(int(m[1]) == int(hasattr(sched, "launches")) for m in meta)
-    # the hub rows (chunked in both) are split between the ranks, none lost
-    assert sum(int(m[0]) for m in meta) == sched.n_splits
+    # the hub rows (chunked in both) are split between the row groups, none lost
+    assert sum(int(m[0]) for m in meta) == F * sched.n_splits

@@ -145,3 +145,4 @@ def test_uncoalesced_edges_fall_back_to_plain_schedule(gpu, force_slices):
     out = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, 3).cpu().numpy()
     ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, 3)
     assert_rows_close(out, np.concatenate([ru, ri]))
+

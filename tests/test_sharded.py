@@ -83,47 +83,58 @@ class CpuShardPlan:
             y[rows] = v
 
 
-def _worker(rank, world, port, kind, K, out_dir):
+def _worker(rank, world, port, kind, K, out_dir, F=1):
     import sys
 
     from conftest import PKG, ROOT
     sys.path[:0] = [str(PKG), str(ROOT), str(ROOT / "tests")]
     import graphs
+    from lgcn_amd.sharded import ShardGrid
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
     U, I, ei = _graph(kind)
+    grid = ShardGrid.build(world, rank, 16, world // F, F)
+    c0, c1 = grid.cols
+    g_r = grid.row_group
     deg = np.bincount(ei[1], minlength=U + I)
-    shards = RowShards.build(deg, U, world)
-    plan = CpuShardPlan(ei, shards, rank)
+    shards = RowShards.build(deg, U, grid.R)
+    plan = CpuShardPlan(ei, shards, g_r)
     uw, iw = graphs.embeddings(U, I, 16, seed=K)
-    x0p = shards.to_padded(torch.from_numpy(uw), torch.from_numpy(iw))
-    ex = BlockExchange(shards, rank)
+    x0p = shards.to_padded(torch.from_numpy(uw[:, c0:c1].copy()), torch.from_numpy(iw[:, c0:c1].copy()))
+    group = grid.exchange_group(dist)
+    ex = BlockExchange(shards, g_r, group) if grid.R > 1 else None
     out = propagate_forward_sharded(x0p, plan, K, ex)
-    a, b = shards.user_rows(rank)
-    c, d = shards.item_rows(rank)
-    np.save(os.path.join(out_dir, f"u{rank}.npy"), out[a:b].numpy())
-    np.save(os.path.join(out_dir, f"i{rank}.npy"), out[c:d].numpy())
+    a, b = shards.user_rows(g_r)
+    c, d = shards.item_rows(g_r)
+    np.save(os.path.join(out_dir, f"u{g_r}_{grid.col_group}.npy"), out[a:b].numpy())
+    np.save(os.path.join(out_dir, f"i{g_r}_{grid.col_group}.npy"), out[c:d].numpy())
     np.save(os.path.join(out_dir, f"log{rank}.npy"), np.array(["".join(x) for x in plan.log]))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,world,K", [("sym", 2, 3), ("sub", 2, 3), ("hub", 2, 4), ("sym", 3, 2),
-                                          ("nonbip", 2, 3), ("sub", 2, 1)])
-def test_sharded_equals_single_rank_bitwise(tmp_path, kind, world, K):
+@pytest.mark.parametrize("kind,world,K,F", [("sym", 2, 3, 1), ("sub", 2, 3, 1), ("hub", 2, 4, 1), ("sym", 3, 2, 1),
+                                            ("nonbip", 2, 3, 1), ("sub", 2, 1, 1), ("sub", 2, 3, 2),
+                                            ("hub", 4, 3, 2), ("nonbip", 4, 2, 2)])
+def test_sharded_equals_single_rank_bitwise(tmp_path, kind, world, K, F):
+    """R = world / F row groups x F column groups (F = 2: each rank propagates 8 of the 16
+    columns; ranks of one column group exchange rows, column groups exchange nothing)."""
     from oracle import c_oracle
 
     port = _free_port()
-    mp.spawn(_worker, args=(world, port, kind, K, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, kind, K, str(tmp_path), F), nprocs=world, join=True)
     import graphs
 
     U, I, ei = _graph(kind)
     uw, iw = graphs.embeddings(U, I, 16, seed=K)
     ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
-    got_u = np.concatenate([np.load(tmp_path / f"u{r}.npy") for r in range(world)])
-    got_i = np.concatenate([np.load(tmp_path / f"i{r}.npy") for r in range(world)])
+    R = world // F
+    got_u = np.concatenate([np.concatenate([np.load(tmp_path / f"u{r}_{c}.npy") for c in range(F)], axis=1)
+                            for r in range(R)])
+    got_i = np.concatenate([np.concatenate([np.load(tmp_path / f"i{r}_{c}.npy") for c in range(F)], axis=1)
+                            for r in range(R)])
     assert np.array_equal(got_u, ru) and np.array_equal(got_i, ri)
     log = list(np.load(tmp_path / "log0.npy"))
     if kind != "nonbip":
@@ -164,3 +175,17 @@ def test_balanced_bounds():
     assert list(balanced_bounds(np.ones(10), 5)) == [0, 2, 4, 6, 8, 10]
     b = balanced_bounds(np.ones(2), 4)  # more ranks than rows: some ranges are empty
     assert b[0] == 0 and b[-1] == 2 and len(b) == 5 and np.all(np.diff(b) >= 0)
+
+
+def test_grid_shape():
+    from lgcn_amd.sharded import ShardGrid, grid_shape
+
+    assert grid_shape(1, 64) == (1, 1)
+    assert grid_shape(2, 64) == (1, 2) and grid_shape(4, 64) == (2, 2) and grid_shape(8, 64) == (4, 2)
+    assert grid_shape(3, 64) == (3, 1)                       # odd world: rows only
+    assert grid_shape(8, 32) == (8, 1)                       # 16 columns would not cut gather requests
+    assert grid_shape(8, 256) == (4, 2)
+    g = ShardGrid.build(8, 5, 64)
+    assert (g.R, g.F, g.row_group, g.col_group, g.cols) == (4, 2, 2, 1, (32, 64))
+    with pytest.raises(ValueError):
+        ShardGrid.build(8, 0, 64, 3, 2)
