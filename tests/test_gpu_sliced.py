@@ -146,3 +146,4 @@ def test_uncoalesced_edges_fall_back_to_plain_schedule(gpu, force_slices):
     ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, 3)
     assert_rows_close(out, np.concatenate([ru, ri]))
 
+
