@@ -130,7 +130,7 @@ def cpu_share():
     return aff, quota, phys
 
 
-def cpu_baseline(graph, K, d, seconds_budget=20.0):
+def cpu_baseline(graph, K, d, seconds_budget=20.0, label="C2"):
     """Reference CPU path (torch primitives of PyG 2.4.0 LGConv, oracle/lgconv_torch.py) on the
     WHOLE C2 edge set, with every CPU of the affinity mask; when a cgroup quota
     caps the process below that, the quota's thread count is timed too and the faster is kept."""
@@ -172,9 +172,9 @@ def cpu_baseline(graph, K, d, seconds_budget=20.0):
             "affinity_cpus": aff, "cgroup_cpu_quota": quota, "physical_cores_machine": phys,
             "threads_timed": {str(k): K * ei.shape[1] / v[0] for k, v in runs.items()},
             "csr_spmm": {"value": K * ei.shape[1] / tc, "unit": "edges/s", "cores": threads,
-                         "sample": f"all {ei.shape[1]} C2 edges, K={K} d={d}: gcn_norm-weighted CSR built once, "
+                         "sample": f"all {ei.shape[1]} {label} edges, K={K} d={d}: gcn_norm-weighted CSR built once, "
                                    f"torch.sparse.mm per layer + layer mean, median of 3"},
-            "sample": f"all {ei.shape[1]} C2 edges (no sampling), all {graph.num_nodes} nodes, K={K} d={d} forward: "
+            "sample": f"all {ei.shape[1]} {label} edges (no sampling), all {graph.num_nodes} nodes, K={K} d={d} forward: "
                       f"index_select -> mul -> scatter_add_ with gcn_norm per layer (PyG 2.4.0 LGConv op sequence, "
                       f"torch {torch.__version__} CPU), median of {reps}"}
 
@@ -428,8 +428,20 @@ def main():
     if exchange is not None:
         result["exchange"] = {"all_gathers_per_step": 2 * (K - 1),
                               "MB_received_per_rank_per_step": exchange.bytes / args.steps / 1e6}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not c5:
-        result["cpu_baseline"] = cpu_baseline(graph, K, d)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if c5:
+            # C5 does not fit a CPU run: the same generator at 1/100 scale (5e6 edges), K and d of C5
+            del ei, user_w, item_w
+            torch.cuda.empty_cache()
+            from lgcn_amd.synth import BipartiteGraph
+
+            sc = 0.01 * args.scale
+            su, si = int(synth.C5_USERS * sc), int(synth.C5_ITEMS * sc)
+            sample = synth.bipartite_device(su, si, int(synth.C5_PAIRS * sc), seed=0, device=dev).cpu().numpy()
+            result["cpu_baseline"] = cpu_baseline(BipartiteGraph(su, si, sample), K, d_full, seconds_budget=10.0,
+                                                  label=f"C5-generator-at-1/100-scale ({su} x {si})")
+        else:
+            result["cpu_baseline"] = cpu_baseline(graph, K, d)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if distributed:
