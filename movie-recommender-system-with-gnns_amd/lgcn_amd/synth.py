@@ -127,7 +127,9 @@ def planted_ml25m(communities: int = 1024, p_in: float = 0.8, scale: float = 1.0
     taste communities, for judging the partitioner at C3 scale: user u is in a random community,
     item i in community i % k; each of u's draws (Zipf-skewed activity, as ``ml25m_shaped``) is,
     with probability p_in, a uniform item of u's community, else an item by global Zipf
-    popularity. Returns (graph, ground-truth community per node)."""
+    popularity. Up to P pairs: heavy users saturate their community's items, and the draw stops
+    after 12 rounds (full scale: 12,447,700 of 12,450,000). Returns (graph, ground-truth
+    community per node)."""
     rng = np.random.default_rng(seed)
     U = max(2, int(ML25M_USERS * scale))
     I = max(2, int(ML25M_ITEMS * scale))

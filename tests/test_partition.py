@@ -79,3 +79,19 @@ def test_partition_recovers_planted_bipartite_communities():
     assert sizes.max() - sizes.min() <= 1
     q, t = cluster.intra_fraction(g.edge_index, part), cluster.intra_fraction(g.edge_index, truth)
     assert q >= 0.9 * t, (q, t)
+
+
+def test_cluster_batches_union_of_parts():
+    """cluster_batches: every batch is the union of parts_per_batch parts' intra-part edges, every
+    intra-part edge lands in exactly one batch, in the parts' seeded order."""
+    from lgcn_amd import cluster, synth
+
+    g = synth.bipartite(600, 300, 6000, seed=4)
+    part, f, batches = cluster.cluster_batches(g.edge_index, g.num_nodes, 16, 4)
+    assert len(batches) == 4 and 0 < f < 1
+    lists = cluster.intra_part_edges(g.edge_index, part, 16)
+    order = np.random.default_rng(1).permutation(16)
+    for b, ei in enumerate(batches):
+        want = np.concatenate([lists[p] for p in order[4 * b:4 * b + 4]], axis=1)
+        assert np.array_equal(ei, want)
+    assert sum(b.shape[1] for b in batches) == int(round(f * g.num_edges))
