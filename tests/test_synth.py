@@ -49,5 +49,6 @@ def test_planted_ml25m_small_scale():
     ei = g.edge_index
     assert np.all((ei[0] < g.num_users) != (ei[1] < g.num_users))
     assert truth.shape == (g.num_nodes,) and truth.max() < 64
-    # most pairs stay inside the planted communities (p_in = 0.8 before deduplication)
-    assert np.mean(truth[ei[0]] == truth[ei[1]]) > 0.3
+    # far more pairs inside the planted communities than chance (1/64); at this scale a community
+    # holds ~9 items, so heavy users saturate it and deduplication drops most inside draws
+    assert np.mean(truth[ei[0]] == truth[ei[1]]) > 0.1
