@@ -263,6 +263,8 @@ int lgcn_copy_scale(const float* x_lo, const float* x_hi, int64_t x_split, int64
  *   (u, U+p, U+n). add == 0 writes every row as (sum * mul) / div (0 where empty) — with the
  *   LightGCN backward scale this is the seed g of the backward; add != 0 only adds (sum * mul) / div
  *   to rows with contributions. */
+/* cw may be NULL: the reg rows are then not materialised (lgcn_reg_rows_add and the scatters'
+ * reg sources form their sums from W). */
 int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split,
                    const float* w_lo, const float* w_hi, int64_t w_split, int64_t U,
                    const int64_t* u, const int64_t* p, const int64_t* n, int64_t B, int32_t d,
@@ -284,10 +286,16 @@ int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C
  * negatives' reg-gradient rows must land after the backward). *overflow (nullable, caller-zeroed)
  * is set if a workgroup's list overflowed — parked sums would then be split; callers check it.
  * store_unless (nullable, uint8[rows]): a row with store_unless[row] == 0 is STORED (not added
- * to) — the row-lazy step leaves rows outside its touched set unwritten. */
+ * to) — the row-lazy step leaves rows outside its touched set unwritten.
+ * The second source may instead be the BPR reg-gradient rows themselves (reg_w_lo non-NULL, C2
+ * NULL): every occurrence of row r contributes kreg * W[r], kreg = reg_coeff * 2 / (reg_B * d)
+ * (the k_bpr_fused expression, reference utils/train_test.py:38-41), so the parked sum is the n
+ * occurrences' copies added in sequence — no [B, d] reg table is read. W: the layer-0 tables
+ * split at reg_w_split. */
 int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
                            int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
-                           const float* C2, float* c2buf, uint8_t* c2flag, int32_t* overflow,
+                           const float* C2, const float* reg_w_lo, const float* reg_w_hi, int64_t reg_w_split,
+                           float reg_coeff, int64_t reg_B, float* c2buf, uint8_t* c2flag, int32_t* overflow,
                            const uint8_t* store_unless, lgcn_stream_t stream);
 /* The same per-row work as lgcn_range_scatter_add (flags, b-order sums, parked C2 sums, store or
  * add) for LARGE B, where every range-scatter workgroup streaming all B keys would cost O(B^2):
@@ -298,8 +306,17 @@ int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_
  * utils/train_test.py:128-134 (compute_embeddings' item_embedding gathers). */
 int lgcn_sorted_scatter_add(const int64_t* rowptr, const int32_t* perm, int64_t nrows, int64_t key_offset,
                             const float* C, int32_t d, float* out_lo, float* out_hi, int64_t split, float mul,
-                            float div, const float* C2, float* c2buf, uint8_t* c2flag, const uint8_t* store_unless,
-                            lgcn_stream_t stream);
+                            float div, const float* C2, const float* reg_w_lo, const float* reg_w_hi,
+                            int64_t reg_w_split, float reg_coeff, int64_t reg_B, float* c2buf, uint8_t* c2flag,
+                            const uint8_t* store_unless, lgcn_stream_t stream);
+/* The fixed (user, positive) reg-gradient rows of a batch: rowptr counts the contributions per
+ * row (a segment plan of the 2B keys); every listed row with n > 0 gets out[r] += n copies of
+ * kreg * W[r] added in sequence (kreg as in lgcn_range_scatter_add). rows (device int32[n_rows],
+ * nullable): the rows to visit (NULL: rows 0 .. n_rows-1). Replaces a [2B, d] reg table and its
+ * ADD pass (reference utils/train_test.py:38-41, the reg term's gradient). */
+int lgcn_reg_rows_add(const int64_t* rowptr, const int32_t* rows, int64_t n_rows, const float* w_lo, const float* w_hi,
+                      int64_t w_split, int32_t d, float coeff, int64_t B, float* out_lo, float* out_hi, int64_t split,
+                      lgcn_stream_t stream);
 int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, const float* c2buf,
                           const uint8_t* c2flag, int32_t d, float* out_lo, float* out_hi, int64_t split,
                           lgcn_stream_t stream);

@@ -26,6 +26,38 @@ __device__ __forceinline__ T* srow(T* lo, T* hi, int64_t split, int64_t r, int64
     return (r < split) ? lo + r * stride : hi + (r - split) * stride;
 }
 
+// The reg-gradient rows of the BPR loss (reference utils/train_test.py:38-41: reg = coeff *
+// mean(eu^2 + ep^2 + en^2) over the layer-0 rows) are kreg * W[row] for every occurrence of a row,
+// kreg = coeff * 2 / (B * d): all the rows summed into one output row are the SAME row. So their
+// sum needs no materialised [3B, d] table: it is n copies of kreg * W[row] added in sequence.
+struct RegSrc {
+    const float* w_lo;  // nullptr: no reg rows
+    const float* w_hi;
+    int64_t w_split;
+    float coeff;
+    int64_t B;
+};
+
+__device__ __forceinline__ float reg_scale(float coeff, int64_t B, int32_t d) {
+    // the same float expression as k_bpr_fused's kreg
+    return coeff * 2.0f / (static_cast<float>(B) * static_cast<float>(d));
+}
+
+// acc = (((0 + v) + v) + ...) n times, v = kreg * W[row]: lane l's NV float4 slots
+template <int LPR, int NV>
+__device__ __forceinline__ void reg_sum(const RegSrc& r, int64_t row, int32_t d, int64_t n, int l, float4 (&acc)[NV]) {
+    const float kreg = reg_scale(r.coeff, r.B, d);
+    const float4* w = reinterpret_cast<const float4*>(row < r.w_split ? r.w_lo + row * d : r.w_hi + (row - r.w_split) * d) + l;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const float4 x = w[k * LPR];
+        const float4 v = make_float4(kreg * x.x, kreg * x.y, kreg * x.z, kreg * x.w);
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int64_t i = 0; i < n; ++i) s = make_float4(s.x + v.x, s.y + v.y, s.z + v.z, s.w + v.w);
+        acc[k] = s;
+    }
+}
+
 template <int LPR>
 __device__ __forceinline__ float group_sum(float v) {
 #pragma unroll
@@ -119,9 +151,9 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
     float4* cfu = reinterpret_cast<float4*>(a.cf + b * d) + l;
     float4* cfp = reinterpret_cast<float4*>(a.cf + (a.B + b) * d) + l;
     float4* cfn = reinterpret_cast<float4*>(a.cf + (2 * a.B + b) * d) + l;
-    float4* cwu = reinterpret_cast<float4*>(a.cw + b * d) + l;
-    float4* cwp = reinterpret_cast<float4*>(a.cw + (a.B + b) * d) + l;
-    float4* cwn = reinterpret_cast<float4*>(a.cw + (2 * a.B + b) * d) + l;
+    float4* cwu = a.cw ? reinterpret_cast<float4*>(a.cw + b * d) + l : nullptr;
+    float4* cwp = a.cw ? reinterpret_cast<float4*>(a.cw + (a.B + b) * d) + l : nullptr;
+    float4* cwn = a.cw ? reinterpret_cast<float4*>(a.cw + (2 * a.B + b) * d) + l : nullptr;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         float4 du, dp, dn;
@@ -137,9 +169,11 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
         cfu[k * LPR] = du;
         cfp[k * LPR] = dp;
         cfn[k * LPR] = dn;
-        cwu[k * LPR] = make_float4(kreg * WU[k].x, kreg * WU[k].y, kreg * WU[k].z, kreg * WU[k].w);
-        cwp[k * LPR] = make_float4(kreg * WP[k].x, kreg * WP[k].y, kreg * WP[k].z, kreg * WP[k].w);
-        cwn[k * LPR] = make_float4(kreg * WN[k].x, kreg * WN[k].y, kreg * WN[k].z, kreg * WN[k].w);
+        if (a.cw != nullptr) {  // materialised reg rows (else the scatters form them, RegSrc)
+            cwu[k * LPR] = make_float4(kreg * WU[k].x, kreg * WU[k].y, kreg * WU[k].z, kreg * WU[k].w);
+            cwp[k * LPR] = make_float4(kreg * WP[k].x, kreg * WP[k].y, kreg * WP[k].z, kreg * WP[k].w);
+            cwn[k * LPR] = make_float4(kreg * WN[k].x, kreg * WN[k].y, kreg * WN[k].z, kreg * WN[k].w);
+        }
     }
     if (l == 0) {
         a.terms[b] = sp;
@@ -253,10 +287,12 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                                                             int64_t span, int64_t key_offset, const float* __restrict__ C,
                                                             int32_t d, float* out_lo, float* out_hi, int64_t split,
                                                             float mul, float div, const float* __restrict__ C2,
+                                                            RegSrc reg,
                                                             float* __restrict__ c2buf, uint8_t* __restrict__ c2flag,
                                                             int* __restrict__ overflow,
                                                             const uint8_t* __restrict__ store_unless) {
     constexpr int GPB = kRSBlock / LPR;
+    const bool second = C2 != nullptr || reg.w_lo != nullptr;  // a second (parked) sum per row
     __shared__ int lkey[kRangeCap];
     __shared__ int lidx[kRangeCap];
     __shared__ int wave_cnt[kRSWaves];
@@ -286,7 +322,7 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                 const int64_t bj = base + (int64_t(wv) * kRSChunks + j) * 64 + lane;
                 kv[j] = bj < B ? keys[bj] : -1;
                 // keys no workgroup owns (outside [0, nrows)): workgroup 0 clears their flag
-                if (C2 && blockIdx.x == 0 && bj < B && (kv[j] < 0 || kv[j] >= nrows)) c2flag[bj] = 0;
+                if (second && blockIdx.x == 0 && bj < B && (kv[j] < 0 || kv[j] >= nrows)) c2flag[bj] = 0;
             }
 #pragma unroll
             for (int j = 0; j < kRSChunks; ++j) {
@@ -331,7 +367,7 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                     break;
                 }
             // every b is in exactly one list: its flag is written here (1 = the row's parked C2 sum)
-            if (C2 && l == 0) c2flag[lidx[e]] = first ? 1 : 0;
+            if (second && l == 0) c2flag[lidx[e]] = first ? 1 : 0;
             if (!first) continue;
             float4 acc[NV], acc2[NV];
 #pragma unroll
@@ -339,8 +375,10 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                 acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
                 acc2[k] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
+            int64_t occ = 0;
             for (int q = e; q < n; ++q) {
                 if (lkey[q] != key) continue;
+                ++occ;
                 const float4* c = reinterpret_cast<const float4*>(C + int64_t(lidx[q]) * d) + l;
 #pragma unroll
                 for (int k = 0; k < NV; ++k) {
@@ -356,12 +394,13 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                     }
                 }
             }
-            if (C2) {  // second source: park the row's sum in the slot of its first occurrence
+            const int64_t row = lo + key + key_offset;
+            if (second) {  // second source: park the row's sum in the slot of its first occurrence
+                if (!C2) reg_sum<LPR, NV>(reg, row, d, occ, l, acc2);
                 float4* cb = reinterpret_cast<float4*>(c2buf + int64_t(lidx[e]) * d) + l;
 #pragma unroll
                 for (int k = 0; k < NV; ++k) cb[k * LPR] = acc2[k];
             }
-            const int64_t row = lo + key + key_offset;
             float4* o = reinterpret_cast<float4*>(srow(out_lo, out_hi, split, row, int64_t(d))) + l;
             if (store_unless && !store_unless[row]) {  // row not written before: store
 #pragma unroll
@@ -395,10 +434,11 @@ __global__ __launch_bounds__(kBlock) void k_sorted_scatter(const int64_t* __rest
                                                            const int32_t* __restrict__ perm, int64_t nrows,
                                                            int64_t key_offset, const float* __restrict__ C, int32_t d,
                                                            float* out_lo, float* out_hi, int64_t split, float mul,
-                                                           float div, const float* __restrict__ C2,
+                                                           float div, const float* __restrict__ C2, RegSrc reg,
                                                            float* __restrict__ c2buf, uint8_t* __restrict__ c2flag,
                                                            const uint8_t* __restrict__ store_unless) {
     constexpr int GPB = kBlock / LPR;
+    const bool second = C2 != nullptr || reg.w_lo != nullptr;
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
     const int64_t r = int64_t(blockIdx.x) * GPB + g;
@@ -406,7 +446,7 @@ __global__ __launch_bounds__(kBlock) void k_sorted_scatter(const int64_t* __rest
     const int64_t q0 = rowptr[r], q1 = rowptr[r + 1];
     if (q0 == q1) return;
     const int64_t first = perm[q0];
-    if (C2)
+    if (second)
         for (int64_t q = q0 + l; q < q1; q += LPR) c2flag[perm[q]] = (q == q0) ? 1 : 0;
     float4 acc[NV], acc2[NV];
 #pragma unroll
@@ -433,12 +473,13 @@ __global__ __launch_bounds__(kBlock) void k_sorted_scatter(const int64_t* __rest
                 acc2[k] = make_float4(acc2[k].x + v2[k].x, acc2[k].y + v2[k].y, acc2[k].z + v2[k].z, acc2[k].w + v2[k].w);
         }
     }
-    if (C2) {
+    const int64_t row = r + key_offset;
+    if (second) {
+        if (!C2) reg_sum<LPR, NV>(reg, row, d, q1 - q0, l, acc2);
         float4* cb = reinterpret_cast<float4*>(c2buf + first * d) + l;
 #pragma unroll
         for (int k = 0; k < NV; ++k) cb[k * LPR] = acc2[k];
     }
-    const int64_t row = r + key_offset;
     float4* o = reinterpret_cast<float4*>(srow(out_lo, out_hi, split, row, int64_t(d))) + l;
     if (store_unless && !store_unless[row]) {
 #pragma unroll
@@ -478,8 +519,8 @@ __global__ __launch_bounds__(kBlock) void k_flagged_rows_add(const int64_t* __re
 
 template <int LPR, int NV>
 int launch_rs(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C, int32_t d, float* lo,
-              float* hi, int64_t split, float mul, float div, const float* C2, float* c2buf, uint8_t* c2flag,
-              int* overflow, const uint8_t* store_unless, hipStream_t s) {
+              float* hi, int64_t split, float mul, float div, const float* C2, RegSrc reg, float* c2buf,
+              uint8_t* c2flag, int* overflow, const uint8_t* store_unless, hipStream_t s) {
     // every workgroup streams all B keys once; enough workgroups that each keeps ~<= 256 entries
     // on average (the list holds kRangeCap), at least 256 (one per CU)
     int64_t wgs = B / 256 + 1;
@@ -489,20 +530,55 @@ int launch_rs(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset,
     const int64_t span = (nrows + wgs - 1) / wgs;
     const int64_t grid = (nrows + span - 1) / span;
     k_range_scatter<LPR, NV><<<dim3(static_cast<unsigned>(grid)), kRSBlock, 0, s>>>(keys, B, nrows, span, key_offset, C, d,
-                                                                                 lo, hi, split, mul, div, C2, c2buf,
-                                                                                 c2flag, overflow, store_unless);
+                                                                                 lo, hi, split, mul, div, C2, reg,
+                                                                                 c2buf, c2flag, overflow, store_unless);
     return check_launch("k_range_scatter");
 }
 
 template <int LPR, int NV>
 int launch_ss(const int64_t* rowptr, const int32_t* perm, int64_t nrows, int64_t key_offset, const float* C, int32_t d,
-              float* lo, float* hi, int64_t split, float mul, float div, const float* C2, float* c2buf,
+              float* lo, float* hi, int64_t split, float mul, float div, const float* C2, RegSrc reg, float* c2buf,
               uint8_t* c2flag, const uint8_t* store_unless, hipStream_t s) {
     constexpr int GPB = kBlock / LPR;
     const int64_t blocks = (nrows + GPB - 1) / GPB;
     k_sorted_scatter<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(
-        rowptr, perm, nrows, key_offset, C, d, lo, hi, split, mul, div, C2, c2buf, c2flag, store_unless);
+        rowptr, perm, nrows, key_offset, C, d, lo, hi, split, mul, div, C2, reg, c2buf, c2flag, store_unless);
     return check_launch("k_sorted_scatter");
+}
+
+// Rows of a segment plan (rowptr over N rows, n contributions to row r): out[r] += n copies of
+// kreg * W[r] summed in sequence — the fixed (user, positive) reg-gradient rows, added after the
+// backward (reference utils/train_test.py:38-41 through autograd), without a [2B, d] table.
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_reg_rows(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ rows,
+                                                     int64_t n_rows, RegSrc reg, int32_t d, float* out_lo,
+                                                     float* out_hi, int64_t split) {
+    constexpr int GPB = kBlock / LPR;
+    const int64_t i = int64_t(blockIdx.x) * GPB + threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
+    if (i >= n_rows) return;
+    const int64_t r = rows ? rows[i] : i;
+    const int64_t n = rowptr[r + 1] - rowptr[r];
+    if (n == 0) return;
+    float4 acc[NV];
+    reg_sum<LPR, NV>(reg, r, d, n, l, acc);
+    float4* o = reinterpret_cast<float4*>(srow(out_lo, out_hi, split, r, int64_t(d))) + l;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const float4 v = o[k * LPR];
+        o[k * LPR] = make_float4(v.x + acc[k].x, v.y + acc[k].y, v.z + acc[k].z, v.w + acc[k].w);
+    }
+}
+
+template <int LPR, int NV>
+int launch_reg(const int64_t* rowptr, const int32_t* rows, int64_t n_rows, RegSrc reg, int32_t d, float* lo, float* hi,
+               int64_t split, hipStream_t s) {
+    constexpr int GPB = kBlock / LPR;
+    const int64_t blocks = (n_rows + GPB - 1) / GPB;
+    if (blocks == 0) return LGCN_OK;
+    k_reg_rows<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(rowptr, rows, n_rows, reg, d, lo, hi,
+                                                                              split);
+    return check_launch("k_reg_rows");
 }
 
 template <int LPR, int NV>
@@ -546,10 +622,10 @@ int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split, const 
                    float* terms, lgcn_stream_t stream) {
     if (B < 0 || d <= 0 || U < 0) return fail(LGCN_E_ARG, "lgcn_bpr_fused: bad sizes");
     if (B == 0) return LGCN_OK;
-    if (!f_lo || !w_lo || !u || !p || !n || !cf || !cw || !terms)
+    if (!f_lo || !w_lo || !u || !p || !n || !cf || !terms)
         return fail(LGCN_E_ARG, "lgcn_bpr_fused: null pointer");
     if (d % 4 != 0 || !al16(f_lo) || !al16(w_lo) || (f_hi && !al16(f_hi)) || (w_hi && !al16(w_hi)) || !al16(cf) ||
-        !al16(cw))
+        (cw && !al16(cw)))
         return fail(LGCN_E_UNSUPPORTED, "lgcn_bpr_fused: needs d %% 4 == 0 and 16-byte aligned rows (d=%d)", d);
     BprArgs a{f_lo, f_hi, f_split, w_lo, w_hi, w_split, U, u, p, n, B, d, touched, div, mul, coeff, cf, cw, terms};
     hipStream_t s = as_stream(stream);
@@ -566,18 +642,23 @@ int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split, const 
 
 int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
                            int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
-                           const float* C2, float* c2buf, uint8_t* c2flag, int32_t* overflow,
+                           const float* C2, const float* reg_w_lo, const float* reg_w_hi, int64_t reg_w_split,
+                           float reg_coeff, int64_t reg_B, float* c2buf, uint8_t* c2flag, int32_t* overflow,
                            const uint8_t* store_unless, lgcn_stream_t stream) {
-    if (B < 0 || d <= 0 || nrows < 0 || (B > 0 && (!keys || !C || !out_lo)) || (C2 && (!c2buf || !c2flag)))
+    const bool second = C2 != nullptr || reg_w_lo != nullptr;
+    if (B < 0 || d <= 0 || nrows < 0 || (B > 0 && (!keys || !C || !out_lo)) || (second && (!c2buf || !c2flag)) ||
+        (C2 && reg_w_lo))
         return fail(LGCN_E_ARG, "lgcn_range_scatter_add: bad args");
     if (B == 0) return LGCN_OK;
     if (nrows == 0)  // no key is in range: nothing to add, every flag 0
-        return C2 ? check_hip(hipMemsetAsync(c2flag, 0, static_cast<size_t>(B), as_stream(stream)), "memset c2flag")
-                  : LGCN_OK;
-    if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C2 && (!al16(C2) || !al16(c2buf))))
+        return second ? check_hip(hipMemsetAsync(c2flag, 0, static_cast<size_t>(B), as_stream(stream)), "memset c2flag")
+                      : LGCN_OK;
+    if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C2 && !al16(C2)) ||
+        (second && !al16(c2buf)) || (reg_w_lo && (!al16(reg_w_lo) || (reg_w_hi && !al16(reg_w_hi)))))
         return fail(LGCN_E_UNSUPPORTED, "lgcn_range_scatter_add: needs d %% 4 == 0 and aligned rows");
     hipStream_t s = as_stream(stream);
-#define LGCN_RS(L, V) launch_rs<L, V>(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, c2buf, c2flag, overflow, store_unless, s)
+    const RegSrc reg{reg_w_lo, reg_w_hi, reg_w_split, reg_coeff, reg_B};
+#define LGCN_RS(L, V) launch_rs<L, V>(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg, c2buf, c2flag, overflow, store_unless, s)
     switch (d) {
         case 16: return LGCN_RS(4, 1);
         case 32: return LGCN_RS(8, 1);
@@ -592,15 +673,20 @@ int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_
 
 int lgcn_sorted_scatter_add(const int64_t* rowptr, const int32_t* perm, int64_t nrows, int64_t key_offset,
                             const float* C, int32_t d, float* out_lo, float* out_hi, int64_t split, float mul,
-                            float div, const float* C2, float* c2buf, uint8_t* c2flag, const uint8_t* store_unless,
-                            lgcn_stream_t stream) {
-    if (nrows < 0 || d <= 0 || (nrows > 0 && (!rowptr || !perm || !C || !out_lo)) || (C2 && (!c2buf || !c2flag)))
+                            float div, const float* C2, const float* reg_w_lo, const float* reg_w_hi,
+                            int64_t reg_w_split, float reg_coeff, int64_t reg_B, float* c2buf, uint8_t* c2flag,
+                            const uint8_t* store_unless, lgcn_stream_t stream) {
+    const bool second = C2 != nullptr || reg_w_lo != nullptr;
+    if (nrows < 0 || d <= 0 || (nrows > 0 && (!rowptr || !perm || !C || !out_lo)) || (second && (!c2buf || !c2flag)) ||
+        (C2 && reg_w_lo))
         return fail(LGCN_E_ARG, "lgcn_sorted_scatter_add: bad args");
     if (nrows == 0) return LGCN_OK;
-    if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C2 && (!al16(C2) || !al16(c2buf))))
+    if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C2 && !al16(C2)) ||
+        (second && !al16(c2buf)) || (reg_w_lo && (!al16(reg_w_lo) || (reg_w_hi && !al16(reg_w_hi)))))
         return fail(LGCN_E_UNSUPPORTED, "lgcn_sorted_scatter_add: needs d %% 4 == 0 and aligned rows");
     hipStream_t s = as_stream(stream);
-#define LGCN_SS(L, V) launch_ss<L, V>(rowptr, perm, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, c2buf, c2flag, store_unless, s)
+    const RegSrc reg{reg_w_lo, reg_w_hi, reg_w_split, reg_coeff, reg_B};
+#define LGCN_SS(L, V) launch_ss<L, V>(rowptr, perm, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg, c2buf, c2flag, store_unless, s)
     switch (d) {
         case 16: return LGCN_SS(4, 1);
         case 32: return LGCN_SS(8, 1);
@@ -611,6 +697,27 @@ int lgcn_sorted_scatter_add(const int64_t* rowptr, const int32_t* perm, int64_t 
         default: return fail(LGCN_E_UNSUPPORTED, "lgcn_sorted_scatter_add: d=%d", d);
     }
 #undef LGCN_SS
+}
+
+int lgcn_reg_rows_add(const int64_t* rowptr, const int32_t* rows, int64_t n_rows, const float* w_lo, const float* w_hi,
+                      int64_t w_split, int32_t d, float coeff, int64_t B, float* out_lo, float* out_hi, int64_t split,
+                      lgcn_stream_t stream) {
+    if (n_rows < 0 || d <= 0 || B < 0 || (n_rows > 0 && (!rowptr || !w_lo || !out_lo)))
+        return fail(LGCN_E_ARG, "lgcn_reg_rows_add: bad args");
+    if (n_rows == 0) return LGCN_OK;
+    if (d % 4 != 0 || !al16(w_lo) || (w_hi && !al16(w_hi)) || !al16(out_lo) || (out_hi && !al16(out_hi)))
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_reg_rows_add: needs d %% 4 == 0 and aligned rows");
+    hipStream_t s = as_stream(stream);
+    const RegSrc reg{w_lo, w_hi, w_split, coeff, B};
+    switch (d) {
+        case 16: return launch_reg<4, 1>(rowptr, rows, n_rows, reg, d, out_lo, out_hi, split, s);
+        case 32: return launch_reg<8, 1>(rowptr, rows, n_rows, reg, d, out_lo, out_hi, split, s);
+        case 64: return launch_reg<16, 1>(rowptr, rows, n_rows, reg, d, out_lo, out_hi, split, s);
+        case 128: return launch_reg<32, 1>(rowptr, rows, n_rows, reg, d, out_lo, out_hi, split, s);
+        case 256: return launch_reg<64, 1>(rowptr, rows, n_rows, reg, d, out_lo, out_hi, split, s);
+        case 512: return launch_reg<64, 2>(rowptr, rows, n_rows, reg, d, out_lo, out_hi, split, s);
+        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_reg_rows_add: d=%d", d);
+    }
 }
 
 int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, const float* c2buf, const uint8_t* c2flag,

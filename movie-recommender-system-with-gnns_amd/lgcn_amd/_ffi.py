@@ -67,10 +67,11 @@ _SIGS = {
                        ctypes.c_int),
     "lgcn_bpr_loss": ([_vp, _i64, _i32, _f32, _vp, _vp], ctypes.c_int),
     "lgcn_segment_rows": ([_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _i32, _f32, _f32, _vp], ctypes.c_int),
-    "lgcn_range_scatter_add": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp,
-                                _vp], ctypes.c_int),
-    "lgcn_sorted_scatter_add": ([_vp, _vp, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp],
-                                ctypes.c_int),
+    "lgcn_range_scatter_add": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _i64,
+                                _f32, _i64, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
+    "lgcn_sorted_scatter_add": ([_vp, _vp, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _i64,
+                                 _f32, _i64, _vp, _vp, _vp, _vp], ctypes.c_int),
+    "lgcn_reg_rows_add": ([_vp, _vp, _i64, _vp, _vp, _i64, _i32, _f32, _i64, _vp, _vp, _i64, _vp], ctypes.c_int),
     "lgcn_adam_consts": ([_vp, _i64, _i64, _f32, ctypes.c_double, ctypes.c_double, _vp], ctypes.c_int),
     "lgcn_row_adam": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64,
                        _vp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _i32, _vp], ctypes.c_int),

@@ -35,6 +35,18 @@ def sliced_chunk(chunk: int) -> int:
 # batch plans (touched-only, segment) use the one-launch block-split schedule; LGCN_BLOCKSPLIT=0
 # keeps them on item pass + combine (A/B knob)
 BLOCK_SPLIT = os.environ.get("LGCN_BLOCKSPLIT", "1") != "0"
+# ... while no split row has more chunks than this: lgcn_spmm_blocksplit sums a split row in one
+# workgroup (16 running sums, csrc/lgcn_spmm.hip kVSums), so a row of c chunks is a chain of
+# ceil(c / 16) chunks — the launch's critical path. Past 2 chunks per running sum (a structured
+# graph's big batches: hub rows with thousands of intra-batch edges) the item pass + combine pair
+# (every chunk in parallel, the same association, so the same bits) is faster.
+BLOCK_SPLIT_MAX_CHUNKS = 32
+
+
+def _block_split_for(splits: torch.Tensor, n_splits: int) -> bool:
+    if not BLOCK_SPLIT:
+        return False
+    return n_splits == 0 or int(splits[:n_splits, 2].max().item()) <= BLOCK_SPLIT_MAX_CHUNKS
 
 
 def slice_bytes_for(num_nodes: int, d: int) -> int:
@@ -134,15 +146,17 @@ def segment_directions(keys: torch.Tensor, N: int, chunk: int = DEFAULT_CHUNK, r
     rowptr = rowptr_b[: N + 1].contiguous()
     val = torch.ones(M, dtype=torch.float32, device=dev)
     mask = (rowptr[1:] > rowptr[:-1]).to(torch.uint8)
-    dense = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, None, stream), chunk, BLOCK_SPLIT)
-    sparse = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, mask, stream), chunk, BLOCK_SPLIT)
+    sd_ = _schedule(rowptr, N, M, chunk, 0, None, stream)
+    dense = CsrDirection(rowptr, col, eid, val, *sd_, chunk, _block_split_for(sd_[1], sd_[3]))
+    ss_ = _schedule(rowptr, N, M, chunk, 0, mask, stream)
+    sparse = CsrDirection(rowptr, col, eid, val, *ss_, chunk, _block_split_for(ss_[1], ss_[3]))
     if int(err.item()):
         raise IndexError("segment keys out of range")
     if row_mask is None:
         return dense, sparse
     # every row of row_mask (0 where it has no contribution), e.g. a batch's touched rows
-    masked = CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, M, chunk, 0, row_mask, stream), chunk,
-                          BLOCK_SPLIT)
+    sm_ = _schedule(rowptr, N, M, chunk, 0, row_mask, stream)
+    masked = CsrDirection(rowptr, col, eid, val, *sm_, chunk, _block_split_for(sm_[1], sm_[3]))
     return dense, sparse, masked
 
 
@@ -183,7 +197,7 @@ def _build_direction(key: torch.Tensor, other: torch.Tensor, N: int, chunk: int,
     del ws, ws2
     # touched-only (Cluster-GCN batch) plans: short chunks, few per split row -> one launch per layer
     return CsrDirection(rowptr, col, eid, val, items, splits, n_items, n_splits, n_partials, chunk,
-                        BLOCK_SPLIT and row_mask is not None), dis, n_bad
+                        row_mask is not None and _block_split_for(splits, n_splits)), dis, n_bad
 
 
 class PropagationPlan:

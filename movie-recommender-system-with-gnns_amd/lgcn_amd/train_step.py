@@ -81,11 +81,16 @@ class _BatchState:
         else:
             self.neg_rowptr = None
         if self.small:
+            # the rows holding (user, positive) keys: lgcn_reg_rows_add visits only these
+            rp = self.fixed_sparse.rowptr
+            self.reg_rows = torch.nonzero(rp[1:] > rp[:-1]).squeeze(1).to(torch.int32).contiguous()
             self.c2buf = torch.empty((B, d), dtype=torch.float32, device=dev)
             self.c2flag = torch.empty(B, dtype=torch.uint8, device=dev)
             self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         self.cf = torch.empty((3 * B, d), dtype=torch.float32, device=dev)
-        self.cw = torch.empty((3 * B, d), dtype=torch.float32, device=dev)
+        # reg-gradient rows: materialised only for the large-batch sort path; the segment-plan path
+        # forms their sums from the layer-0 rows (lgcn_reg_rows_add, the scatters' reg source)
+        self.cw = None if self.small else torch.empty((3 * B, d), dtype=torch.float32, device=dev)
         self.terms = torch.empty(2 * B, dtype=torch.float32, device=dev)
         self.loss = torch.empty(1, dtype=torch.float32, device=dev)
         self.rowptr = torch.empty(N + 1, dtype=torch.int64, device=dev)
@@ -108,14 +113,17 @@ def sorted_scatter_min_b() -> int:
     return int(os.environ.get("LGCN_SORTED_SCATTER_MIN_B", 49152))
 
 
-def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: float, store_unless, stream) -> None:
-    """dF rows of the step's negatives into the gradient tables, their reg rows parked per row
-    (first-occurrence slot, st.c2flag) for lgcn_flagged_rows_add after the backward."""
+def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: float, store_unless, stream,
+                      uw, iw, coeff: float) -> None:
+    """dF rows of the step's negatives into the gradient tables, their reg rows' sums (formed from
+    the layer-0 rows uw / iw) parked per row (first-occurrence slot, st.c2flag) for
+    lgcn_flagged_rows_add after the backward."""
     B = st.B
-    C, C2 = st.cf[2 * B:], st.cw[2 * B:]
+    C = st.cf[2 * B:]
+    reg = (None, uw.data_ptr(), iw.data_ptr(), U, coeff, B)
     if st.neg_rowptr is None:
         _ffi.check(lib.lgcn_range_scatter_add(st.neg.data_ptr(), B, I, U, C.data_ptr(), d, gu.data_ptr(), gi.data_ptr(),
-                                              U, mul, div, C2.data_ptr(), st.c2buf.data_ptr(), st.c2flag.data_ptr(),
+                                              U, mul, div, *reg, st.c2buf.data_ptr(), st.c2flag.data_ptr(),
                                               st.overflow.data_ptr(), _ffi.ptr(store_unless), stream),
                    "lgcn_range_scatter_add")
         return
@@ -123,9 +131,16 @@ def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: 
                                   st.neg_col.data_ptr(), st.neg_perm.data_ptr(), st.neg_err.data_ptr(),
                                   st.neg_ws.data_ptr(), st.neg_ws.numel(), stream), "lgcn_csr_build(negatives)")
     _ffi.check(lib.lgcn_sorted_scatter_add(st.neg_rowptr.data_ptr(), st.neg_perm.data_ptr(), I, U, C.data_ptr(), d,
-                                           gu.data_ptr(), gi.data_ptr(), U, mul, div, C2.data_ptr(),
+                                           gu.data_ptr(), gi.data_ptr(), U, mul, div, *reg,
                                            st.c2buf.data_ptr(), st.c2flag.data_ptr(), _ffi.ptr(store_unless), stream),
                "lgcn_sorted_scatter_add")
+
+
+def add_fixed_reg_rows(lib, st, gu, gi, U: int, N: int, d: int, uw, iw, coeff: float, stream) -> None:
+    """The (user, positive) reg-gradient rows: n copies of kreg * W[r] per row with n keys."""
+    _ffi.check(lib.lgcn_reg_rows_add(st.fixed_sparse.rowptr.data_ptr(), st.reg_rows.data_ptr(), st.reg_rows.numel(),
+                                     uw.data_ptr(), iw.data_ptr(), U, d, coeff, st.B, gu.data_ptr(), gi.data_ptr(), U,
+                                     stream), "lgcn_reg_rows_add")
 
 
 class FusedTrainStep:
@@ -194,7 +209,7 @@ class FusedTrainStep:
             _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
                                           st.users.data_ptr(), st.pos.data_ptr(), st.neg.data_ptr(), B, d,
                                           st.plan.touched.data_ptr(), div, mul,
-                                          self.coeff, st.cf.data_ptr(), st.cw.data_ptr(), st.terms.data_ptr(),
+                                          self.coeff, st.cf.data_ptr(), _ffi.ptr(st.cw), st.terms.data_ptr(),
                                           stream), "lgcn_bpr_fused")
             _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(), stream),
                        "lgcn_bpr_loss")
@@ -208,9 +223,9 @@ class FusedTrainStep:
                 spmm(st.fixed_dense, N, d, (st.cf, None, big), None, grads, None, _ffi.EPI_SCALE, div, mul,
                      stream=stream)
                 # negatives: dF rows into g now, their reg rows parked (per row, first-occurrence slot)
-                scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, None, stream)
+                scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, None, stream, uw, iw, self.coeff)
                 propagate_backward_seeded(gu, gi, st.plan, K)
-                spmm(st.fixed_sparse, N, d, (st.cw, None, big), None, grads, None, _ffi.EPI_ADD, stream=stream)
+                add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, self.coeff, stream)
                 _ffi.check(lib.lgcn_flagged_rows_add(st.neg.data_ptr(), B, U, st.c2buf.data_ptr(),
                                                      st.c2flag.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U,
                                                      stream), "lgcn_flagged_rows_add")
@@ -261,7 +276,7 @@ class FusedTrainStep:
             _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
                                           st.users.data_ptr(), st.pos.data_ptr(), st.neg.data_ptr(), B, d,
                                           st.plan.touched.data_ptr(), div, mul,
-                                          self.coeff, st.cf.data_ptr(), st.cw.data_ptr(), st.terms.data_ptr(),
+                                          self.coeff, st.cf.data_ptr(), _ffi.ptr(st.cw), st.terms.data_ptr(),
                                           stream), "lgcn_bpr_fused")
             _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(), stream),
                        "lgcn_bpr_loss")
@@ -271,9 +286,9 @@ class FusedTrainStep:
             spmm(st.fixed_touched, N, d, (st.cf, None, big), None, grads, None, _ffi.EPI_SCALE, div, mul,
                  stream=stream)
             # ... the negatives' rows added (stored where the row is outside the touched set)
-            scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream)
+            scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream, uw, iw, self.coeff)
             propagate_backward_seeded(gu, gi, st.plan, K)
-            spmm(st.fixed_sparse, N, d, (st.cw, None, big), None, grads, None, _ffi.EPI_ADD, stream=stream)
+            add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, self.coeff, stream)
             _ffi.check(lib.lgcn_flagged_rows_add(st.neg.data_ptr(), B, U, st.c2buf.data_ptr(),
                                                  st.c2flag.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U,
                                                  stream), "lgcn_flagged_rows_add")

@@ -55,14 +55,16 @@ def _run(gpu, keys_np, nrows, off, d, N, mul, div, with_c2=True, seed=0, sorted_
                                       perm.data_ptr(), err.data_ptr(), ws.data_ptr(), ws.numel(), s), "csr")
         _ffi.check(lib.lgcn_sorted_scatter_add(rowptr.data_ptr(), perm.data_ptr(), nrows, off, Cg.data_ptr(), d,
                                                lo.data_ptr(), hi.data_ptr(), split, mul, div,
-                                               C2g.data_ptr() if with_c2 else None, buf.data_ptr(), flag.data_ptr(),
-                                               _ffi.ptr(su), s), "lgcn_sorted_scatter_add")
+                                               C2g.data_ptr() if with_c2 else None, None, None, 0, 0.0, 0,
+                                               buf.data_ptr(), flag.data_ptr(), _ffi.ptr(su), s),
+                   "lgcn_sorted_scatter_add")
         assert int(err.item()) == 0
     else:
         _ffi.check(lib.lgcn_range_scatter_add(keys.data_ptr(), B, nrows, off, Cg.data_ptr(), d, lo.data_ptr(),
                                               hi.data_ptr(), split, mul, div,
-                                              C2g.data_ptr() if with_c2 else None, buf.data_ptr(), flag.data_ptr(),
-                                              ovf.data_ptr(), _ffi.ptr(su), s), "lgcn_range_scatter_add")
+                                              C2g.data_ptr() if with_c2 else None, None, None, 0, 0.0, 0,
+                                              buf.data_ptr(), flag.data_ptr(), ovf.data_ptr(), _ffi.ptr(su), s),
+                   "lgcn_range_scatter_add")
     after1 = torch.cat([lo, hi]).cpu().numpy()
     if with_c2:
         _ffi.check(lib.lgcn_flagged_rows_add(keys.data_ptr(), B, off, buf.data_ptr(), flag.data_ptr(), d,
@@ -147,3 +149,89 @@ def test_sorted_scatter_bitwise_range_scatter(gpu, B, nrows, d):
                 np.testing.assert_array_equal(after1, r1)
                 np.testing.assert_array_equal(after2, r2)
                 np.testing.assert_array_equal(flag, rflag)
+
+
+def _kreg(coeff, B, d):
+    # k_bpr_fused's float expression: coeff * 2.0f / (float(B) * float(d))
+    return np.float32(np.float32(coeff) * np.float32(2.0)) / (np.float32(B) * np.float32(d))
+
+
+@pytest.mark.parametrize("sorted_", [False, True])
+@pytest.mark.parametrize("B,nrows,d", [(3000, 500, 64), (20000, 59047, 128), (5000, 40, 32)])
+def test_reg_source_equals_materialised_reg_rows(gpu, sorted_, B, nrows, d):
+    """The scatters' reg source (every occurrence of row r contributes kreg * W[r], formed on the
+    fly) parks bitwise the sums a materialised C2 = kreg * W[key] table gives (same values in the
+    same order), range and sorted paths; lgcn_reg_rows_add == n copies added in sequence."""
+    from lgcn_amd import _ffi
+
+    lib = _ffi.load()
+    rng = np.random.default_rng(B + d)
+    keys_np = rng.integers(0, nrows, B)
+    off = 7
+    N = off + nrows + 1
+    W = (rng.standard_normal((N, d)) * 0.1).astype(np.float32)
+    coeff = 5e-3
+    kreg = _kreg(coeff, B, d)
+    C2 = (kreg * W[off + keys_np]).astype(np.float32)
+    s = _ffi.stream_of(gpu)
+    keys = torch.from_numpy(keys_np.astype(np.int64)).to(gpu)
+    C = torch.from_numpy(rng.standard_normal((B, d)).astype(np.float32)).to(gpu)
+    Wg = torch.from_numpy(W).to(gpu)
+    split = off + nrows // 2
+    res = []
+    for mode in ("table", "reg"):
+        out = torch.zeros((N, d), device=gpu)
+        buf = torch.zeros((B, d), device=gpu)
+        flag = torch.zeros(B, dtype=torch.uint8, device=gpu)
+        c2 = torch.from_numpy(C2).to(gpu) if mode == "table" else None
+        reg = (None, Wg[:split].data_ptr(), Wg[split:].data_ptr(), split, coeff, B) if mode == "reg" else \
+              (c2.data_ptr(), None, None, 0, 0.0, 0)
+        if sorted_:
+            rowptr = torch.empty(nrows + 1, dtype=torch.int64, device=gpu)
+            col = torch.empty(B, dtype=torch.int32, device=gpu)
+            perm = torch.empty(B, dtype=torch.int32, device=gpu)
+            err = torch.zeros(1, dtype=torch.int64, device=gpu)
+            nb = _ffi._sz(0)
+            _ffi.check(lib.lgcn_csr_workspace_size(B, nrows, nb), "ws")
+            ws = torch.empty(max(1, nb.value), dtype=torch.uint8, device=gpu)
+            _ffi.check(lib.lgcn_csr_build(keys.data_ptr(), keys.data_ptr(), B, nrows, rowptr.data_ptr(),
+                                          col.data_ptr(), perm.data_ptr(), err.data_ptr(), ws.data_ptr(), ws.numel(),
+                                          s), "csr")
+            _ffi.check(lib.lgcn_sorted_scatter_add(rowptr.data_ptr(), perm.data_ptr(), nrows, off, C.data_ptr(), d,
+                                                   out[:split].data_ptr(), out[split:].data_ptr(), split, 1.0, 1.0,
+                                                   *reg, buf.data_ptr(), flag.data_ptr(), None, s), "sorted")
+        else:
+            ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+            _ffi.check(lib.lgcn_range_scatter_add(keys.data_ptr(), B, nrows, off, C.data_ptr(), d,
+                                                  out[:split].data_ptr(), out[split:].data_ptr(), split, 1.0, 1.0,
+                                                  *reg, buf.data_ptr(), flag.data_ptr(), ovf.data_ptr(), None, s),
+                       "range")
+            assert int(ovf.item()) == 0
+        res.append((out.cpu(), buf.cpu(), flag.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][2], res[1][2])
+    fl = res[0][2].bool()
+    assert torch.equal(res[0][1][fl], res[1][1][fl])
+    # lgcn_reg_rows_add over the keys' CSR: n copies of kreg * W[r], added in sequence
+    counts = np.bincount(keys_np, minlength=nrows)
+    rowptr = torch.zeros(N + 1, dtype=torch.int64)
+    rowptr[off + 1:off + nrows + 1] = torch.from_numpy(np.cumsum(counts))
+    rowptr[off + nrows + 1:] = int(counts.sum())
+    out = torch.from_numpy(W).to(gpu).clone()
+    _ffi.check(lib.lgcn_reg_rows_add(rowptr.to(gpu).data_ptr(), None, N, Wg[:split].data_ptr(), Wg[split:].data_ptr(),
+                                     split, d, coeff, B, out[:split].data_ptr(), out[split:].data_ptr(), split, s),
+               "reg_rows")
+    # the same through an explicit row list (every row with contributions, descending order)
+    listed = torch.from_numpy((off + np.flatnonzero(counts))[::-1].astype(np.int32).copy()).to(gpu)
+    out2 = torch.from_numpy(W).to(gpu).clone()
+    _ffi.check(lib.lgcn_reg_rows_add(rowptr.to(gpu).data_ptr(), listed.data_ptr(), listed.numel(), Wg[:split].data_ptr(),
+                                     Wg[split:].data_ptr(), split, d, coeff, B, out2[:split].data_ptr(),
+                                     out2[split:].data_ptr(), split, s), "reg_rows listed")
+    assert torch.equal(out, out2)
+    want = W.copy()
+    for r in np.flatnonzero(counts):
+        v = (kreg * W[off + r]).astype(np.float32)
+        acc = np.zeros(d, np.float32)
+        for _ in range(counts[r]):
+            acc = (acc + v).astype(np.float32)
+        want[off + r] = (want[off + r] + acc).astype(np.float32)
+    assert np.array_equal(out.cpu().numpy(), want)
