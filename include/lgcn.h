@@ -430,7 +430,8 @@ int lgcn_rows_accumulate(const int64_t* ids, const float* rows, int64_t world, i
 /* ---------------------------------------------------------------------------------------
  * Host-side (no GPU): balanced k-way node partition for Cluster-GCN batching, the METIS
  * replacement for PyG ClusterData (reference data/dataset_handler.py:273). Deterministic
- * restreaming Linear Deterministic Greedy over the undirected adjacency of (src[e], dst[e]);
+ * restreaming Linear Deterministic Greedy over the undirected adjacency of (src[e], dst[e]) —
+ * of the nodes, and of size-constrained label-propagation clusters (the better result kept);
  * part_out[N] receives ids in [0, num_parts); `imbalance` is the streaming capacity slack and a
  * final fix-up leaves every part with exactly floor or ceil(N/num_parts) nodes. Host pointers. Errors: lgcn_partition_last_error(). */
 int lgcn_partition_edges(const int64_t* src, const int64_t* dst, int64_t E, int64_t N,
