@@ -77,11 +77,15 @@ def test_epoch_matches_oracle_harness(gpu, cpu_negatives):
         opt = torch.optim.Adam(m.parameters(), lr=1e-3)
         cpu_negatives(9)
         loss = TT.train(m, opt, [_Batch(x) for x in batches], dev)
-        res[name] = (loss, m.user_embedding.weight.detach().cpu().numpy())
+        st = opt.state[m.user_embedding.weight]
+        res[name] = (loss, m.user_embedding.weight.detach().cpu().numpy(), st["exp_avg"].cpu().numpy(),
+                     st["exp_avg_sq"].cpu().numpy())
     assert abs(res["hip"][0] - res["ref"][0]) <= 1e-5 * abs(res["ref"][0])
-    # Adam's first steps move each weight by ~lr * sign(grad): compare with that scale in mind
-    diff = np.abs(res["hip"][1] - res["ref"][1])
-    assert np.mean(diff <= 1e-6) > 0.999 and diff.max() <= 2.1e-3
+    # three Adam steps: weights and first moments within 1e-5 of their scale, every element
+    # (measured: 6.4e-8 on weights of max 0.04, 4.0e-8 on moments of max 5.2e-3)
+    w_ref, m_ref = res["ref"][1], res["ref"][2]
+    assert np.abs(res["hip"][1] - w_ref).max() <= 1e-5 * np.abs(w_ref).max()
+    assert np.abs(res["hip"][2] - m_ref).max() <= 1e-5 * np.abs(m_ref).max()
 
 
 def test_cluster_training_converges_on_gpu(gpu):
@@ -307,6 +311,8 @@ def test_lazy_train_step_matches_dense_step(gpu, use_graphs, clip, whole):
         return
     for a, b in zip(res[0][0], res[1][0]):
         assert abs(a - b) <= 1e-5 * max(1.0, abs(a))
+    # the clip norm's summation order differs (row norms vs the dense two-pass norm), and 20 Adam
+    # steps at lr 1e-2 amplify it; measured 1.8e-4 (user table) and 1.4e-5 (item table) of the max
     for x, y in ((res[0][1], res[1][1]), (res[0][2], res[1][2])):
         assert (x - y).abs().max().item() <= 1e-3 * x.abs().max().item()
 
