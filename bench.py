@@ -221,8 +221,10 @@ def main():
     ap.add_argument("--chunk", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", default=None,
-                    help="c2, N > 1: RxF grid (R row groups x F column groups, R*F = N); default "
-                         "lgcn_amd.sharded.grid_shape (two column groups when N is even and d/2 >= 32)")
+                    help="c2, N > 1: RxF grid (R row groups x F column groups, R*F = N); default: every "
+                         "lgcn_amd.sharded.grid_candidates grid is timed for a few steps and the fastest runs")
+    ap.add_argument("--exchange-mode", choices=["allgather", "p2p"], default="allgather",
+                    help="c2 with --shard and R > 1: one all_gather per block, or sends to every peer")
     ap.add_argument("--workload", choices=["propagate", "train"], default="propagate",
                     help="propagate: C2 headline (default); train: C3/C4 Cluster-GCN training steps")
     ap.add_argument("--parts", type=int, default=1024, help="train: Cluster-GCN parts")
@@ -298,30 +300,72 @@ def main():
     item_w = (torch.randn(I, d, device=dev, generator=gen) * 0.01).contiguous()
     t0 = time.perf_counter()
     exchange = None
+    grid_trials = None
     if sharded:
-        from lgcn_amd.sharded import BlockExchange, RowShards, ShardedPlan, ShardGrid, propagate_forward_sharded
+        from lgcn_amd.sharded import (BlockExchange, RowShards, ShardedPlan, ShardGrid, grid_candidates,
+                                      propagate_forward_sharded)
 
-        R, F = (int(v) for v in args.shard.split("x")) if args.shard else (None, None)
-        grid = ShardGrid.build(world, rank, d_full, R, F)
+        in_deg = np.bincount(graph.edge_index[1], minlength=N)
+        groups = {}
+
+        def build_grid(R, F, mode):
+            """This rank's share of an R x F grid: plan, layer-0 columns, exchange, step."""
+            grid = ShardGrid.build(world, rank, d_full, R, F)
+            c0, c1 = grid.cols
+            shards = RowShards.build(in_deg, U, grid.R)
+            splan = ShardedPlan(ei, shards, grid.row_group, c1 - c0, chunk)
+            x0p = shards.to_padded(user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous())
+            if (grid.R, grid.F) not in groups:  # collective: every rank creates the column groups
+                groups[(grid.R, grid.F)] = grid.exchange_group(dist)
+            ex = (BlockExchange(shards, grid.row_group, groups[(grid.R, grid.F)], grid.members, mode or "allgather")
+                  if grid.R > 1 else None)
+            return dict(grid=grid, shards=shards, splan=splan, ex=ex, mode=mode if grid.R > 1 else None,
+                        step=lambda: propagate_forward_sharded(x0p, splan, K, ex))
+
+        def trial_ms(st, n=8):
+            """max-over-ranks ms per step of a candidate grid (untimed by the bench line)."""
+            with torch.no_grad():
+                for _ in range(2):
+                    st["step"]()
+                torch.cuda.synchronize()
+                dist.barrier()
+                t = time.perf_counter()
+                for _ in range(n):
+                    st["step"]()
+                torch.cuda.synchronize()
+                t = torch.tensor([(time.perf_counter() - t) / n * 1e3], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+
+        if args.shard:
+            R, F = (int(v) for v in args.shard.split("x"))
+            st = build_grid(R, F, args.exchange_mode)
+        else:
+            # the grid is picked by measurement: the compute per rank is known on one GPU
+            # (tools/shard_rank_probe.py), the exchange cost only on the node's xGMI links
+            st, best, grid_trials = None, None, {}
+            for R, F, mode in grid_candidates(world, d_full):
+                cand = build_grid(R, F, mode)
+                ms = trial_ms(cand)
+                grid_trials[f"{R}x{F}" + (f"/{mode}" if mode else "")] = round(ms, 4)
+                log(f"[rank {rank}] grid trial {R}x{F} {mode or ''}: {ms:.3f} ms per step")
+                if best is None or ms < best:
+                    st, best = cand, ms
+                else:
+                    del cand
+                torch.cuda.empty_cache()
+        del user_w, item_w
+        grid, shards, splan, exchange, step = st["grid"], st["shards"], st["splan"], st["ex"], st["step"]
         c0, c1 = grid.cols
         d = c1 - c0
         g_r = grid.row_group
-        shards = RowShards.build(np.bincount(graph.edge_index[1], minlength=N), U, grid.R)
-        splan = ShardedPlan(ei, shards, g_r, d, chunk, slice_d=d_full)
-        x0p = shards.to_padded(user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous())
-        del user_w, item_w
-        group = grid.exchange_group(dist)  # collective: every rank creates the column groups
-        exchange = BlockExchange(shards, g_r, group) if grid.R > 1 else None
         scheds = [h.direction for h in splan.halves]
         torch.cuda.synchronize()
         ua, ub_ = shards.user_rows(g_r)
         ia, ib_ = shards.item_rows(g_r)
-        log(f"[rank {rank}] grid {grid.R}x{grid.F}: row group {g_r} (users {ub_ - ua} of {U}, items {ib_ - ia} of "
-            f"{I}), columns [{c0}, {c1}); padded N {shards.NP}; {'sliced' if splan.sliced else 'plain'} halves, "
-            f"{time.perf_counter() - t0:.2f} s")
-
-        def step():
-            return propagate_forward_sharded(x0p, splan, K, exchange)
+        log(f"[rank {rank}] grid {grid.R}x{grid.F}{' ' + st['mode'] if st['mode'] else ''}: row group {g_r} "
+            f"(users {ub_ - ua} of {U}, items {ib_ - ia} of {I}), columns [{c0}, {c1}); padded N {shards.NP}; "
+            f"{'sliced' if splan.sliced else 'plain'} halves, {time.perf_counter() - t0:.2f} s")
     else:
         # side_split = U: rows gathering the item table run first, then rows gathering the user table
         plan = PropagationPlan(ei, N, chunk, side_split=U)
@@ -410,10 +454,12 @@ def main():
                                    "no collective") if c5 else
                                   (f"{grid.R} row groups x {grid.F} column groups over {world} GPUs: each rank "
                                    f"propagates {d} of {d_full} columns of one edge-balanced destination row range "
-                                   f"(whole graph and whole column share of the table on every rank); ranks of a column "
-                                   f"group all_gather (RCCL) each exchanged layer's two row blocks, each overlapped "
-                                   f"with the other half-layer; column groups exchange nothing; bitwise the 1-GPU "
-                                   f"result" if sharded else "single GPU")},
+                                   f"(whole graph and whole column share of the table on every rank); " +
+                                   (f"ranks of a column group exchange each exchanged layer's two row blocks "
+                                    f"({args.dist_backend} {'all_gather' if st['mode'] == 'allgather' else 'sends to every peer'}"
+                                    f"), each overlapped with the other half-layer; " if grid.R > 1 else "") +
+                                   "column groups exchange nothing; bitwise the 1-GPU result of its schedule"
+                                   if sharded else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "basis": basis,
                      "kernel": (f"k_spmm_vec<{kernel_lpr(d)},sliced> (lgcn_spmm_run_slices, {launches} source-slice "
@@ -425,8 +471,10 @@ def main():
                      "effective_GBps": alg_launch / (kernel_ms * 1e-3) / 1e9},
         "cpu_baseline": None,
     }
+    if grid_trials is not None:
+        result["config"]["grid_trials_ms_per_step"] = grid_trials
     if exchange is not None:
-        result["exchange"] = {"all_gathers_per_step": 2 * (K - 1),
+        result["exchange"] = {"mode": exchange.mode, "block_exchanges_per_step": 2 * (K - 1),
                               "MB_received_per_rank_per_step": exchange.bytes / args.steps / 1e6}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if c5:

@@ -112,77 +112,146 @@ __device__ __forceinline__ void finish_row_vec(const SpmmArgs& a, int64_t r, int
     }
 }
 
-// Sum of one item's edges into acc, in CSR order. Per 16-edge (LPR-edge) batch the lanes load
-// (col, val) coalesced — the NEXT batch's pair is loaded before the current batch's gathers are
-// issued, so that latency overlaps them — then UNROLL neighbour rows are gathered (one float4 per
-// lane each) before the first add, and added in CSR order.
+// One batch of n <= LPR edges of an item, added to acc in CSR order: lane j of the group holds
+// edge j's (col, val), broadcast with __shfl; UNROLL neighbour rows are gathered (one float4 per
+// lane each) before the first add.
 template <int LPR, int NV, int UNROLL, int TAIL>
-__device__ __forceinline__ void sum_item(const SpmmArgs& a, const lgcn_item_t it, int l, float4 (&acc)[NV]) {
+__device__ __forceinline__ void sum_batch(const float4* __restrict__ xlo, const float4* __restrict__ xhi,
+                                          int64_t x_split, int c, float w, int n, float4 (&acc)[NV]) {
     const int64_t d4 = int64_t(LPR) * NV;
-    const float4* __restrict__ xlo = reinterpret_cast<const float4*>(a.x_lo) + l;
-    const float4* __restrict__ xhi = reinterpret_cast<const float4*>(a.x_hi) + l;
-    int cn = 0;
-    float wn = 0.f;
-    if (l < it.len) {
-        cn = *(a.col + it.beg + l);
-        wn = *(a.val + it.beg + l);
-    }
-    for (int b = 0; b < it.len; b += LPR) {
-        const int n = min(LPR, it.len - b);
-        const int c = cn;
-        const float w = wn;
-        if (b + LPR < it.len && l < it.len - b - LPR) {  // prefetch the next batch
-            cn = *(a.col + it.beg + b + LPR + l);
-            wn = *(a.val + it.beg + b + LPR + l);
-        }
-        int j = 0;
-        for (; j + UNROLL <= n; j += UNROLL) {
-            float4 xv[UNROLL][NV];
-            float wv[UNROLL];
+    int j = 0;
+    for (; j + UNROLL <= n; j += UNROLL) {
+        float4 xv[UNROLL][NV];
+        float wv[UNROLL];
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const int cj = __shfl(c, j + u, LPR);
-                wv[u] = __shfl(w, j + u, LPR);
-                const float4* src = (cj < a.x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - a.x_split) * d4;
+        for (int u = 0; u < UNROLL; ++u) {
+            const int cj = __shfl(c, j + u, LPR);
+            wv[u] = __shfl(w, j + u, LPR);
+            const float4* src = (cj < x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - x_split) * d4;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) xv[u][k] = src[k * LPR];
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wv[u], xv[u][k]);
+    }
+    if (TAIL == 1 && j < n) {
+        // the batch's last n - j (< UNROLL) edges: all their gathers issued (exec-predicated)
+        // before the first add, then added in CSR order — one memory latency instead of n - j
+        const int rem = n - j;
+        float4 xv[UNROLL - 1][NV];
+        float wv[UNROLL - 1];
+#pragma unroll
+        for (int u = 0; u < UNROLL - 1; ++u) {
+            const int ju = j + (u < rem ? u : 0);
+            const int cj = __shfl(c, ju, LPR);
+            wv[u] = __shfl(w, ju, LPR);
+            const float4* src = (cj < x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - x_split) * d4;
+            if (u < rem) {
 #pragma unroll
                 for (int k = 0; k < NV; ++k) xv[u][k] = src[k * LPR];
             }
+        }
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
+        for (int u = 0; u < UNROLL - 1; ++u)
+            if (u < rem) {
 #pragma unroll
                 for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wv[u], xv[u][k]);
-        }
-        if (TAIL == 1 && j < n) {
-            // the batch's last n - j (< UNROLL) edges: all their gathers issued (exec-predicated)
-            // before the first add, then added in CSR order — one memory latency instead of n - j
-            const int rem = n - j;
-            float4 xv[UNROLL - 1][NV];
-            float wv[UNROLL - 1];
-#pragma unroll
-            for (int u = 0; u < UNROLL - 1; ++u) {
-                const int ju = j + (u < rem ? u : 0);
-                const int cj = __shfl(c, ju, LPR);
-                wv[u] = __shfl(w, ju, LPR);
-                const float4* src = (cj < a.x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - a.x_split) * d4;
-                if (u < rem) {
-#pragma unroll
-                    for (int k = 0; k < NV; ++k) xv[u][k] = src[k * LPR];
-                }
             }
+        j = n;
+    }
+    for (; j < n; ++j) {
+        const int cj = __shfl(c, j, LPR);
+        const float wj = __shfl(w, j, LPR);
+        const float4* src = (cj < x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - x_split) * d4;
 #pragma unroll
-            for (int u = 0; u < UNROLL - 1; ++u)
-                if (u < rem) {
+        for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wj, src[k * LPR]);
+    }
+}
+
+// Rows narrower than UNROLL lanes (LPR < UNROLL, d <= 16): one load round of SB = LPR * CM edges,
+// UNROLL edges at a time across UNROLL / LPR batches (edge e of the round: lane e % LPR of batch
+// slot e / LPR, both static), each group's gathers issued (exec-predicated on e < n) before its
+// adds, which run in CSR order — UNROLL rows in flight per lane group instead of LPR.
+template <int LPR, int NV, int UNROLL, int CM>
+__device__ __forceinline__ void sum_round_narrow(const float4* __restrict__ xlo, const float4* __restrict__ xhi,
+                                                 int64_t x_split, const int (&c)[CM], const float (&w)[CM], int n,
+                                                 float4 (&acc)[NV]) {
+    constexpr int SB = LPR * CM;
+    constexpr int UG = UNROLL < SB ? UNROLL : SB;
+    static_assert(SB % UG == 0, "load round must be a whole number of gather groups");
+    const int64_t d4 = int64_t(LPR) * NV;
 #pragma unroll
-                    for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wv[u], xv[u][k]);
-                }
-            j = n;
+    for (int j = 0; j < SB; j += UG) {
+        if (j >= n) break;
+        float4 xv[UG][NV];
+        float wv[UG];
+#pragma unroll
+        for (int u = 0; u < UG; ++u) {
+            const int e = j + u;
+            const int cj = __shfl(c[e / LPR], e % LPR, LPR);
+            wv[u] = __shfl(w[e / LPR], e % LPR, LPR);
+            if (e < n) {
+                const float4* src = (cj < x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - x_split) * d4;
+#pragma unroll
+                for (int k = 0; k < NV; ++k) xv[u][k] = src[k * LPR];
+            }
         }
-        for (; j < n; ++j) {
-            const int cj = __shfl(c, j, LPR);
-            const float wj = __shfl(w, j, LPR);
-            const float4* src = (cj < a.x_split) ? xlo + int64_t(cj) * d4 : xhi + (int64_t(cj) - a.x_split) * d4;
 #pragma unroll
-            for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wj, src[k * LPR]);
+        for (int u = 0; u < UG; ++u)
+            if (j + u < n) {
+#pragma unroll
+                for (int k = 0; k < NV; ++k) acc[k] = f4_axpy(acc[k], wv[u], xv[u][k]);
+            }
+    }
+}
+
+// Sum of one item's edges into acc, in CSR order. The lanes load (col, val) coalesced, CM batches
+// of LPR edges per load round (CM > 1 at narrow rows: one 128-B line of col per round instead of a
+// fraction of one, which the gathers would evict from L1 before the next batch reads it) — the
+// NEXT round's pairs are loaded before the current round's gathers are issued, so that latency
+// overlaps them — then each batch goes through sum_batch in order.
+template <int LPR, int NV, int UNROLL, int TAIL, int CM = 1>
+__device__ __forceinline__ void sum_item(const SpmmArgs& a, const lgcn_item_t it, int l, float4 (&acc)[NV]) {
+    const float4* __restrict__ xlo = reinterpret_cast<const float4*>(a.x_lo) + l;
+    const float4* __restrict__ xhi = reinterpret_cast<const float4*>(a.x_hi) + l;
+    constexpr int SB = LPR * CM;  // edges per load round
+    int cn[CM];
+    float wn[CM];
+#pragma unroll
+    for (int m = 0; m < CM; ++m) {
+        cn[m] = 0;
+        wn[m] = 0.f;
+        if (m * LPR + l < it.len) {
+            cn[m] = *(a.col + it.beg + m * LPR + l);
+            wn[m] = *(a.val + it.beg + m * LPR + l);
+        }
+    }
+    for (int b = 0; b < it.len; b += SB) {
+        int c[CM];
+        float w[CM];
+#pragma unroll
+        for (int m = 0; m < CM; ++m) {
+            c[m] = cn[m];
+            w[m] = wn[m];
+        }
+        if (b + SB < it.len) {  // prefetch the next round
+#pragma unroll
+            for (int m = 0; m < CM; ++m)
+                if (b + SB + m * LPR + l < it.len) {
+                    cn[m] = *(a.col + it.beg + b + SB + m * LPR + l);
+                    wn[m] = *(a.val + it.beg + b + SB + m * LPR + l);
+                }
+        }
+        if constexpr (LPR < UNROLL) {
+            sum_round_narrow<LPR, NV, UNROLL, CM>(xlo, xhi, a.x_split, c, w, min(SB, it.len - b), acc);
+        } else {
+#pragma unroll
+            for (int m = 0; m < CM; ++m)
+                if (b + m * LPR < it.len)
+                    sum_batch<LPR, NV, UNROLL, TAIL>(xlo, xhi, a.x_split, c[m], w[m], min(LPR, it.len - b - m * LPR),
+                                                     acc);
         }
     }
 }
@@ -198,7 +267,7 @@ constexpr int kVSums = 16;
 // each chunk (from 0, in CSR order — the partial the item pass would have written) into its
 // running sum, then the sums in order through LDS: the association of item pass + k_combine_vec,
 // so bitwise the same result, without the partials' round trip or the second launch.
-template <int LPR, int NV, int UNROLL, int TAIL>
+template <int LPR, int NV, int UNROLL, int TAIL, int CM>
 __device__ __forceinline__ void split_row_block(const SpmmArgs& a, int64_t s, int g, int l) {
     constexpr int GPB = kBlock / LPR;
     constexpr int VPG = (kVSums + GPB - 1) / GPB;
@@ -215,7 +284,7 @@ __device__ __forceinline__ void split_row_block(const SpmmArgs& a, int64_t s, in
             float4 part[NV];
 #pragma unroll
             for (int k = 0; k < NV; ++k) part[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-            sum_item<LPR, NV, UNROLL, TAIL>(a, a.chunks[int64_t(sp.pbeg) + c], l, part);
+            sum_item<LPR, NV, UNROLL, TAIL, CM>(a, a.chunks[int64_t(sp.pbeg) + c], l, part);
 #pragma unroll
             for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], part[k]);
         }
@@ -239,13 +308,13 @@ __device__ __forceinline__ void split_row_block(const SpmmArgs& a, int64_t s, in
 // running sum from a.run unless it is the row's FIRST segment, and runs the epilogue only on its
 // LAST one; the sum stays one sequential chain in CSR order across launches.
 // BSPLIT: workgroups [0, n_splits) sum the split rows (split_row_block), the rest the items.
-template <int LPR, int NV, int UNROLL, bool SLICED = false, int TAIL = 0, bool BSPLIT = false>
+template <int LPR, int NV, int UNROLL, bool SLICED = false, int TAIL = 0, bool BSPLIT = false, int CM = 1>
 __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
     constexpr int GPB = kBlock / LPR;
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
     if (BSPLIT && int64_t(blockIdx.x) < a.n_splits) {
-        split_row_block<LPR, NV, UNROLL, TAIL>(a, blockIdx.x, g, l);
+        split_row_block<LPR, NV, UNROLL, TAIL, CM>(a, blockIdx.x, g, l);
         return;
     }
     const int64_t item = (int64_t(blockIdx.x) - (BSPLIT ? a.n_splits : 0)) * GPB + g;
@@ -266,7 +335,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
 #pragma unroll
         for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    sum_item<LPR, NV, UNROLL, TAIL>(a, it, l, acc);
+    sum_item<LPR, NV, UNROLL, TAIL, CM>(a, it, l, acc);
     if (it.dst < 0) {
         float4* p = reinterpret_cast<float4*>(a.partial) + int64_t(-it.dst - 1) * d4 + l;
 #pragma unroll
@@ -410,13 +479,13 @@ __global__ __launch_bounds__(kBlock) void k_combine_scalar(SpmmArgs a) {
 
 enum { PASS_ITEMS = 1, PASS_COMBINE = 2, PASS_BOTH = 3, PASS_BSPLIT = 4 };
 
-template <int LPR, int NV, int UNROLL, int TAIL = 0>
+template <int LPR, int NV, int UNROLL, int TAIL = 0, int CM = 1>
 int launch_vec(const SpmmArgs& a, hipStream_t s, int pass) {
     constexpr int GPB = kBlock / LPR;
     if (pass == PASS_BSPLIT) {  // split rows (one workgroup each) and items in one launch
         const int64_t blocks = a.n_splits + (a.n_items + GPB - 1) / GPB;
         if (blocks > 0) {
-            k_spmm_vec<LPR, NV, UNROLL, false, TAIL, true><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+            k_spmm_vec<LPR, NV, UNROLL, false, TAIL, true, CM><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
             if (int rc = check_launch("k_spmm_vec")) return rc;
         }
         return LGCN_OK;
@@ -424,9 +493,9 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass) {
     if ((pass & PASS_ITEMS) && a.n_items > 0) {
         const int64_t blocks = (a.n_items + GPB - 1) / GPB;
         if (a.run != nullptr)
-            k_spmm_vec<LPR, NV, UNROLL, true, TAIL><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+            k_spmm_vec<LPR, NV, UNROLL, true, TAIL, false, CM><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
         else
-            k_spmm_vec<LPR, NV, UNROLL, false, TAIL><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+            k_spmm_vec<LPR, NV, UNROLL, false, TAIL, false, CM><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
         if (int rc = check_launch("k_spmm_vec")) return rc;
     }
     if ((pass & PASS_COMBINE) && a.n_splits > 0) {
@@ -455,6 +524,12 @@ int launch_scalar(const SpmmArgs& a, hipStream_t s, int pass) {
         if (int rc = check_launch("k_combine_scalar")) return rc;
     }
     return LGCN_OK;
+}
+
+// Index-load-round override for A/B tuning (LGCN_SPMM_CM; 0 = default choice).
+int spmm_cm() {
+    const char* v = std::getenv("LGCN_SPMM_CM");
+    return v ? std::atoi(v) : 0;
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -520,13 +595,39 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
         // LGCN_SPMM_VARIANT (A/B knob): 1 = 16-deep unroll at d=64, 2 = tail on, 3 = tail off.
         const int v = spmm_variant();
         const bool tail = v == 2 || (v != 1 && v != 3 && (d <= 64 || (run == nullptr && n_items <= 65536)));
+        // Index load rounds (CM batches of LPR edges per col/val load): one or two 128-B lines of
+        // col per round at narrow rows, on every launch but the block-split Cluster-GCN batch plans
+        // (at d = 128 the C3 step measured +11 % with CM = 4, so d >= 128 keeps one batch per round).
+        // Measured (profiles/r02x_cm/): C2 K=3 d=64 1.317 -> 1.269 ms (CM 4), d=32 0.791 -> 0.742
+        // (CM 4), d=16 0.859 -> 0.610 (CM 16), d=8 1.354 -> 0.773 (CM 32); d=128/256 slower (kept at 1).
+        // The narrow-row round path at d=32 measured the same as per-batch (0.739 vs 0.743 ms), at d=64
+        // +5 %. LGCN_SPMM_CM overrides.
+        const bool rounds = pass != PASS_BSPLIT;
+        const int cm = spmm_cm();
         if (tail) {
             switch (d) {
-                case 4: return launch_vec<1, 1, 8, 1>(a, s, pass);
-                case 8: return launch_vec<2, 1, 8, 1>(a, s, pass);
-                case 16: return launch_vec<4, 1, 8, 1>(a, s, pass);
-                case 32: return launch_vec<8, 1, 8, 1>(a, s, pass);
-                case 64: return launch_vec<16, 1, 8, 1>(a, s, pass);
+                case 4: return (cm ? cm : rounds ? 32 : 8) == 32 ? launch_vec<1, 1, 8, 1, 32>(a, s, pass)
+                                                                : launch_vec<1, 1, 8, 1, 8>(a, s, pass);
+                case 8: {
+                    const int c = cm ? cm : rounds ? 32 : 4;
+                    return c == 16 ? launch_vec<2, 1, 8, 1, 16>(a, s, pass)
+                         : c == 32 ? launch_vec<2, 1, 8, 1, 32>(a, s, pass) : launch_vec<2, 1, 8, 1, 4>(a, s, pass);
+                }
+                case 16: {
+                    const int c = cm ? cm : rounds ? 16 : 2;
+                    return c == 8 ? launch_vec<4, 1, 8, 1, 8>(a, s, pass)
+                         : c == 16 ? launch_vec<4, 1, 8, 1, 16>(a, s, pass) : launch_vec<4, 1, 8, 1, 2>(a, s, pass);
+                }
+                case 32: {
+                    const int c = cm ? cm : rounds ? 4 : 1;
+                    return c == 4 ? launch_vec<8, 1, 8, 1, 4>(a, s, pass)
+                         : c == 8 ? launch_vec<8, 1, 8, 1, 8>(a, s, pass) : launch_vec<8, 1, 8, 1>(a, s, pass);
+                }
+                case 64: {
+                    const int c = cm ? cm : rounds ? 4 : 1;
+                    return c == 4 ? launch_vec<16, 1, 8, 1, 4>(a, s, pass)
+                         : c == 2 ? launch_vec<16, 1, 8, 1, 2>(a, s, pass) : launch_vec<16, 1, 8, 1>(a, s, pass);
+                }
                 case 128: return launch_vec<32, 1, 8, 1>(a, s, pass);
                 case 256: return launch_vec<64, 1, 8, 1>(a, s, pass);
                 case 512: return launch_vec<64, 2, 4, 1>(a, s, pass);
@@ -535,9 +636,9 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
             }
         }
         switch (d) {
-            case 4: return launch_vec<1, 1, 8>(a, s, pass);
-            case 8: return launch_vec<2, 1, 8>(a, s, pass);
-            case 16: return launch_vec<4, 1, 8>(a, s, pass);
+            case 4: return launch_vec<1, 1, 8, 0, 8>(a, s, pass);
+            case 8: return launch_vec<2, 1, 8, 0, 4>(a, s, pass);
+            case 16: return launch_vec<4, 1, 8, 0, 2>(a, s, pass);
             case 32: return launch_vec<8, 1, 8>(a, s, pass);
             case 64: return v == 1 ? launch_vec<16, 1, 16>(a, s, pass) : launch_vec<16, 1, 8>(a, s, pass);
             case 128: return launch_vec<32, 1, 8>(a, s, pass);

@@ -157,14 +157,33 @@ MIN_COLS = 32  # a column share narrower than 128 B rows stops cutting gather re
 
 
 def grid_shape(world: int, d: int) -> tuple[int, int]:
-    """(R row groups, F column groups), R * F = world. The item pass is bound by gather requests
-    per edge, not bytes: halving a 256-B row to 128 B halves the requests (C2, one GPU: 1.72 ->
-    0.94 ms per K=3 step at d = 64 -> 32, plain schedule), narrower rows do not (d = 16: 1.28 ms).
-    Splitting columns needs no exchange, splitting rows needs an all_gather per layer, so two
-    column groups are used whenever the world is even and d / 2 >= MIN_COLS; the rest are rows."""
+    """(R row groups, F column groups), R * F = world: the fixed shape ShardGrid.build uses when
+    none is given (bench.py instead times every grid_candidates grid and runs the fastest). Two
+    column groups whenever the world is even and d / 2 >= MIN_COLS, the rest rows: columns need
+    no exchange, and a 128-B row is one gather request instead of two (C2, one GPU, K=3:
+    1.27 ms at d = 64, 0.74 at d = 32, 0.61 at d = 16, 0.77 at d = 8, profiles/r02x_cm/)."""
     if world >= 2 and world % 2 == 0 and d % 2 == 0 and d // 2 >= MIN_COLS and (d // 2) % 4 == 0:
         return world // 2, 2
     return world, 1
+
+
+def grid_candidates(world: int, d: int) -> list[tuple[int, int, str | None]]:
+    """(R, F, exchange mode) grids bench.py times before it picks one for a world of ranks: every
+    column split F | world with d / F a multiple of 4 and >= 8, rows-only grids (F = 1) only when
+    no column split exists (they move the most bytes), both exchange modes where a row group has
+    three or more ranks (an all_gather and direct peer sends differ there), none with R = 1."""
+    out = []
+    for F in range(world, 0, -1):
+        if world % F or d % F or (d // F) % 4 or d // F < 8:
+            continue
+        R = world // F
+        if R == 1:
+            out.append((R, F, None))
+        else:
+            out += [(R, F, m) for m in (EXCHANGE_MODES if R >= 3 else EXCHANGE_MODES[:1])]
+    if any(F > 1 for _, F, _ in out):
+        out = [c for c in out if c[1] > 1]
+    return out
 
 
 @dataclasses.dataclass
@@ -200,6 +219,11 @@ class ShardGrid:
         w = self.d // self.F
         return self.col_group * w, (self.col_group + 1) * w
 
+    @property
+    def members(self) -> list[int]:
+        """Global ranks of this rank's column group, in row-group order (the exchange peers)."""
+        return [self.col_group + self.F * i for i in range(self.R)]
+
     def exchange_group(self, dist):
         """The process group of this rank's column group (None = the default group when F = 1).
         Every rank must call this (new_group is collective over the world)."""
@@ -230,8 +254,9 @@ class ShardedPlan:
     def __init__(self, edge_index: torch.Tensor, shards: RowShards, rank: int, d: int, chunk: int | None = None,
                  slice_d: int | None = None):
         """d: the width this rank propagates (its column share); slice_d: the width whose one-GPU
-        slicing decision and bounds are kept (the full d when columns are split too), so every
-        row keeps the one-GPU segments and hub chunks."""
+        slicing decision and bounds are used (default d: the one-GPU plan at the share's width,
+        whose result the share then is bitwise; the full width keeps the full-width segments and
+        hub chunks instead, at 5-15 % more time for narrow shares, profiles/r02x_cm/)."""
         from .plan import DEFAULT_CHUNK, CsrDirection, _build_direction, _schedule, slice_bytes_for, sliced_chunk
         from .sliced import build_sliced, slice_bounds
 
@@ -262,8 +287,9 @@ class ShardedPlan:
                       ("i", "u", torch.from_numpy(shards.owned_mask(rank, "u")).to(dev))]   # B: item sources
         else:
             pieces = [("ui", "ui", owned)]
-        # the one-GPU plan's slicing decision and bounds (lgcn_amd.plan.PropagationPlan.schedule),
-        # mapped to padded ids: the same segments, the same hub chunks
+        # the one-GPU plan's slicing decision and bounds at width slice_d
+        # (lgcn_amd.plan.PropagationPlan.schedule), mapped to padded ids: the same segments, the
+        # same hub chunks
         sd_ = int(slice_d or d)
         sb = slice_bytes_for(N, sd_)
         bounds = slice_bounds(N, U, sd_, sb) if (sb and E) else None
@@ -310,24 +336,46 @@ def _slice_forced() -> bool:
     return os.environ.get("LGCN_SLICE_MB") is not None
 
 
+EXCHANGE_MODES = ("allgather", "p2p")
+
+
 class BlockExchange:
     """all_gather of one block (every rank's user rows, or item rows) of a layer output.
 
-    nccl (RCCL over xGMI): ``all_gather_into_tensor`` in place (each rank's chunk is its slice of
-    the output block), issued on a side stream after an event on the compute stream; the caller's
-    stream waits on the returned event only before the half that reads the block.
-    gloo (tests, rehearsal): the same collective through host memory, synchronously."""
+    nccl (RCCL over xGMI), issued on a side stream after an event on the compute stream; the
+    caller's stream waits on the returned event only before the half that reads the block:
+    * ``allgather``: ``all_gather_into_tensor`` in place (each rank's chunk is its slice of the
+      output block) — RCCL picks the algorithm (rings over the group);
+    * ``p2p``: one send of this rank's chunk to every peer and one receive from every peer, as one
+      ``batch_isend_irecv`` (a group of R ranks drives its R - 1 direct xGMI links at once).
+    gloo (tests, rehearsal): the same exchange through host memory, synchronously."""
 
-    def __init__(self, shards: RowShards, rank: int, group=None):
+    def __init__(self, shards: RowShards, rank: int, group=None, members: list[int] | None = None,
+                 mode: str = "allgather"):
         """rank: this rank's index among the ranks that share its columns (its RowShards rank);
-        group: their process group (None = the default group)."""
+        group: their process group (None = the default group); members: their global ranks in
+        row-group order (p2p; default range(W)); mode: one of EXCHANGE_MODES."""
         import torch.distributed as dist
 
+        if mode not in EXCHANGE_MODES:
+            raise ValueError(f"exchange mode {mode!r} not in {EXCHANGE_MODES}")
         self.dist = dist
-        self.shards, self.rank, self.group = shards, rank, group
+        self.shards, self.rank, self.group, self.mode = shards, rank, group, mode
+        self.members = list(members) if members is not None else list(range(shards.W))
+        if len(self.members) != shards.W:
+            raise ValueError(f"{len(self.members)} exchange members for {shards.W} row groups")
         self.nccl = dist.get_backend(group) == "nccl"
         self.stream = None
         self.bytes = 0  # received per rank, over the run
+
+    def _p2p_ops(self, out, mine, c):
+        d = self.dist
+        ops = []
+        for p, peer in enumerate(self.members):
+            if p != self.rank:
+                ops.append(d.P2POp(d.isend, mine, peer, self.group))
+                ops.append(d.P2POp(d.irecv, out[p * c:(p + 1) * c], peer, self.group))
+        return ops
 
     def start(self, buf: torch.Tensor, b: str):
         lo, c = self.shards.block(b)
@@ -342,12 +390,26 @@ class BlockExchange:
             ready.record(torch.cuda.current_stream(buf.device))
             with torch.cuda.stream(self.stream):
                 self.stream.wait_event(ready)
-                self.dist.all_gather_into_tensor(out, mine, group=self.group)
+                if self.mode == "p2p":
+                    for req in self.dist.batch_isend_irecv(self._p2p_ops(out, mine, c)):
+                        req.wait()
+                else:
+                    self.dist.all_gather_into_tensor(out, mine, group=self.group)
                 done = torch.cuda.Event()
                 done.record(self.stream)
             return done
         host = torch.empty((W * c, buf.shape[1]), dtype=buf.dtype)
-        self.dist.all_gather_into_tensor(host, mine.cpu().clone(), group=self.group)
+        if self.mode == "p2p":
+            host[self.rank * c:(self.rank + 1) * c] = mine.cpu()
+            reqs = []
+            for p, peer in enumerate(self.members):
+                if p != self.rank:
+                    reqs.append(self.dist.isend(host[self.rank * c:(self.rank + 1) * c], peer, group=self.group))
+                    reqs.append(self.dist.irecv(host[p * c:(p + 1) * c], peer, group=self.group))
+            for req in reqs:
+                req.wait()
+        else:
+            self.dist.all_gather_into_tensor(host, mine.cpu().clone(), group=self.group)
         out.copy_(host)
         return None
 

@@ -1,6 +1,9 @@
 """Row-sharded propagation (lgcn_amd.sharded) with the HIP kernels: the sharded K-layer forward is
 BITWISE the one-GPU forward (lgcn_amd.propagate_forward over PropagationPlan(side_split=U)),
 every rank's rows, for the plain and the source-sliced schedules, with hub rows cut into chunks.
+One row group (R = 1) with F column groups: each column share is bitwise the one-GPU forward of
+that share at its own width (a rank slices the source range for its width); R > 1: bitwise the
+full-width one-GPU forward on the plain schedule (its chunks do not depend on the width).
 
 W = 1 runs in this process; W = 2 runs two ranks on the one GPU of the box over gloo (the block
 all_gather goes through host memory; the 8-GPU RCCL run is bench.py --gpus N)."""
@@ -35,9 +38,10 @@ def _graph(kind):
     return graphs.subsampled(U=400, I=300, pairs=6000, seed=2)
 
 
-def _reference(dev, case, R=1):
-    """One-GPU forward with the schedule a rank of R row groups runs: the default one (R = 1), or
-    the plain schedule at lgcn_amd.sharded.rank_chunk (R > 1)."""
+def _reference(dev, case, R=1, F=1):
+    """One-GPU forward with the schedule a rank of R row groups runs: the default one (R = 1; with
+    F column groups, each column share run at its own width), or the plain schedule at
+    lgcn_amd.sharded.rank_chunk (R > 1). Returns (..., out, sched, hub rows over the shares)."""
     from lgcn_amd import propagate_forward
     from lgcn_amd.plan import PropagationPlan
     from lgcn_amd.sharded import rank_chunk
@@ -50,16 +54,20 @@ def _reference(dev, case, R=1):
     saved = os.environ.get("LGCN_SLICE_MB")
     if R > 1:
         os.environ["LGCN_SLICE_MB"] = "0"
+    Fw = F if R == 1 else 1
+    w = d // Fw
     try:
         plan = PropagationPlan(torch.from_numpy(ei).to(dev), U + I, rank_chunk(chunk, R), side_split=U)
-        out = propagate_forward(torch.from_numpy(uw).to(dev), torch.from_numpy(iw).to(dev), plan, K)
-        sched = plan.schedule("fwd", d)
+        outs = [propagate_forward(torch.from_numpy(uw[:, c * w:(c + 1) * w].copy()).to(dev),
+                                  torch.from_numpy(iw[:, c * w:(c + 1) * w].copy()).to(dev), plan, K).cpu().numpy()
+                for c in range(Fw)]
+        sched = plan.schedule("fwd", w)
     finally:
         if saved is None:
             os.environ.pop("LGCN_SLICE_MB", None)
         else:
             os.environ["LGCN_SLICE_MB"] = saved
-    return U, I, ei, uw, iw, out.cpu().numpy(), sched
+    return U, I, ei, uw, iw, np.concatenate(outs, axis=1), sched, F * sched.n_splits
 
 
 def _sharded(dev, case, world, rank, F=1):
@@ -74,8 +82,7 @@ def _sharded(dev, case, world, rank, F=1):
     c0, c1 = grid.cols
     g_r = grid.row_group
     shards = RowShards.build(np.bincount(ei[1], minlength=U + I), U, grid.R)
-    # the column share keeps the full width's slicing, so rows keep the one-GPU segments
-    splan = ShardedPlan(torch.from_numpy(ei).to(dev), shards, g_r, c1 - c0, chunk, slice_d=d)
+    splan = ShardedPlan(torch.from_numpy(ei).to(dev), shards, g_r, c1 - c0, chunk)
     x0p = shards.to_padded(torch.from_numpy(uw[:, c0:c1].copy()).to(dev), torch.from_numpy(iw[:, c0:c1].copy()).to(dev))
     import torch.distributed as dist
 
@@ -92,7 +99,7 @@ def test_sharded_w1_bitwise(gpu, monkeypatch, case):
     slice_mb = CASES[case][4]
     if slice_mb:
         monkeypatch.setenv("LGCN_SLICE_MB", slice_mb)
-    U, I, ei, uw, iw, ref, sched = _reference(gpu, case)
+    U, I, ei, uw, iw, ref, sched, _ = _reference(gpu, case)
     shards, splan, ou, oi = _sharded(gpu, case, 1, 0)
     assert shards.NP == U + I and splan.sliced == hasattr(sched, "launches")
     assert splan.bipartite and len(splan.halves) == 2
@@ -136,13 +143,14 @@ def _worker(rank, world, port, case, out_dir, F=1):
                                                                      ("ml25m5_sliced", 4, 2), ("sub_K2_d128", 4, 2)])
 def test_sharded_ranks_bitwise(gpu, monkeypatch, tmp_path, case, world, F):
     """world / F row groups x F column groups (gloo, every rank on the one GPU): the assembled
-    output is bitwise the one-GPU forward at the full width with the schedule the ranks run
-    (lgcn_amd.sharded.rank_chunk); with R > 1 also within 1e-5 per row of the default one."""
+    output is bitwise the one-GPU forward with the schedule the ranks run (R = 1: each column share
+    at its width; R > 1: lgcn_amd.sharded.rank_chunk at the full width); with R > 1 also within
+    1e-5 per row of the default one."""
     slice_mb = CASES[case][4]
     if slice_mb:
         monkeypatch.setenv("LGCN_SLICE_MB", slice_mb)
     R = world // F
-    U, I, ei, uw, iw, ref, sched = _reference(gpu, case, R)
+    U, I, ei, uw, iw, ref, sched, n_hubs = _reference(gpu, case, R, F)
     torch.cuda.synchronize()
     mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path), F), nprocs=world, join=True)
     got_u = np.concatenate([np.concatenate([np.load(tmp_path / f"u{r}_{c}.npy") for c in range(F)], axis=1)
@@ -158,4 +166,4 @@ def test_sharded_ranks_bitwise(gpu, monkeypatch, tmp_path, case, world, F):
     meta = [np.load(tmp_path / f"n{r}.npy") for r in range(world)]
     assert all(int(m[1]) == int(hasattr(sched, "launches")) for m in meta)
     # the hub rows (chunked in both) are split between the row groups, none lost
-    assert sum(int(m[0]) for m in meta) == F * sched.n_splits
+    assert sum(int(m[0]) for m in meta) == n_hubs

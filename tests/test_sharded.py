@@ -83,7 +83,7 @@ class CpuShardPlan:
             y[rows] = v
 
 
-def _worker(rank, world, port, kind, K, out_dir, F=1):
+def _worker(rank, world, port, kind, K, out_dir, F=1, mode="allgather"):
     import sys
 
     from conftest import PKG, ROOT
@@ -105,7 +105,7 @@ def _worker(rank, world, port, kind, K, out_dir, F=1):
     uw, iw = graphs.embeddings(U, I, 16, seed=K)
     x0p = shards.to_padded(torch.from_numpy(uw[:, c0:c1].copy()), torch.from_numpy(iw[:, c0:c1].copy()))
     group = grid.exchange_group(dist)
-    ex = BlockExchange(shards, g_r, group) if grid.R > 1 else None
+    ex = BlockExchange(shards, g_r, group, grid.members, mode) if grid.R > 1 else None
     out = propagate_forward_sharded(x0p, plan, K, ex)
     a, b = shards.user_rows(g_r)
     c, d = shards.item_rows(g_r)
@@ -115,16 +115,20 @@ def _worker(rank, world, port, kind, K, out_dir, F=1):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,world,K,F", [("sym", 2, 3, 1), ("sub", 2, 3, 1), ("hub", 2, 4, 1), ("sym", 3, 2, 1),
-                                            ("nonbip", 2, 3, 1), ("sub", 2, 1, 1), ("sub", 2, 3, 2),
-                                            ("hub", 4, 3, 2), ("nonbip", 4, 2, 2)])
-def test_sharded_equals_single_rank_bitwise(tmp_path, kind, world, K, F):
+@pytest.mark.parametrize("kind,world,K,F,mode", [("sym", 2, 3, 1, "allgather"), ("sub", 2, 3, 1, "allgather"),
+                                                 ("hub", 2, 4, 1, "allgather"), ("sym", 3, 2, 1, "allgather"),
+                                                 ("nonbip", 2, 3, 1, "allgather"), ("sub", 2, 1, 1, "allgather"),
+                                                 ("sub", 2, 3, 2, "allgather"), ("hub", 4, 3, 2, "allgather"),
+                                                 ("nonbip", 4, 2, 2, "allgather"), ("sym", 3, 2, 1, "p2p"),
+                                                 ("hub", 4, 3, 2, "p2p"), ("sub", 4, 3, 1, "p2p")])
+def test_sharded_equals_single_rank_bitwise(tmp_path, kind, world, K, F, mode):
     """R = world / F row groups x F column groups (F = 2: each rank propagates 8 of the 16
-    columns; ranks of one column group exchange rows, column groups exchange nothing)."""
+    columns; ranks of one column group exchange rows, column groups exchange nothing); the rows
+    travel as one all_gather per block, or as sends to / receives from every peer (p2p)."""
     from oracle import c_oracle
 
     port = _free_port()
-    mp.spawn(_worker, args=(world, port, kind, K, str(tmp_path), F), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, kind, K, str(tmp_path), F, mode), nprocs=world, join=True)
     import graphs
 
     U, I, ei = _graph(kind)
@@ -189,3 +193,16 @@ def test_grid_shape():
     assert (g.R, g.F, g.row_group, g.col_group, g.cols) == (4, 2, 2, 1, (32, 64))
     with pytest.raises(ValueError):
         ShardGrid.build(8, 0, 64, 3, 2)
+
+
+def test_grid_candidates():
+    from lgcn_amd.sharded import grid_candidates
+
+    assert grid_candidates(1, 64) == [(1, 1, None)]
+    assert grid_candidates(2, 64) == [(1, 2, None)]
+    assert grid_candidates(4, 64) == [(1, 4, None), (2, 2, "allgather")]
+    assert grid_candidates(8, 64) == [(1, 8, None), (2, 4, "allgather"), (4, 2, "allgather"), (4, 2, "p2p")]
+    assert grid_candidates(3, 64) == [(3, 1, "allgather"), (3, 1, "p2p")]   # odd world: rows only
+    assert grid_candidates(8, 32) == [(2, 4, "allgather"), (4, 2, "allgather"), (4, 2, "p2p")]  # 4-col shares: no
+    for R, F, _ in grid_candidates(8, 256):
+        assert R * F == 8 and (256 // F) % 4 == 0

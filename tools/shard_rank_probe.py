@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--chunks", default="256")
     ap.add_argument("--plain", action="store_true", help="LGCN_SLICE_MB=0: the plain item schedule")
+    ap.add_argument("--full-slices", action="store_true", help="R = 1 ranks keep the full width's slices")
     args = ap.parse_args()
     if args.plain:
         os.environ["LGCN_SLICE_MB"] = "0"
@@ -41,7 +42,7 @@ def main():
         shards = RowShards.build(deg, U, R)
         times = []
         for gr in sorted({0, R - 1}):
-            splan = ShardedPlan(ei, shards, gr, c1 - c0, chunk, slice_d=d)
+            splan = ShardedPlan(ei, shards, gr, c1 - c0, chunk, slice_d=d if args.full_slices else None)
             x0p = shards.to_padded(uw[:, c0:c1].contiguous(), iw[:, c0:c1].contiguous())
             with torch.no_grad():
                 for _ in range(3):
