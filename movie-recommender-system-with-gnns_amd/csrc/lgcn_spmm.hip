@@ -53,7 +53,25 @@ struct SpmmArgs {
     float mul;
     float* run;  // sliced launches: running row sums between a row's source-slice segments
     const lgcn_item_t* chunks;  // block-split launches: split rows' chunk items, partial-slot order
+    int32_t nt = 0;  // bit 0: non-temporal row stores, bit 1: non-temporal row loads (LGCN_SPMM_NT overrides)
 };
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_row(float4* p, float4 v, int nt) {
+    if (nt & 1) {
+        f4v w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<f4v*>(p));
+    } else {
+        *p = v;
+    }
+}
+__device__ __forceinline__ float4 ld_row(const float4* p, int nt) {
+    if (nt & 2) {
+        const f4v w = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+        return make_float4(w.x, w.y, w.z, w.w);
+    }
+    return *p;
+}
 
 // Sliced-schedule item flags, in the high bits of lgcn_item_t::len (rows, not partial chunks).
 constexpr int32_t kItemFirst = 0x20000000;
@@ -87,12 +105,12 @@ __device__ __forceinline__ void finish_row_vec(const SpmmArgs& a, int64_t r, int
         const float4* e = reinterpret_cast<const float4*>(split_row(a.e_lo, a.e_hi, a.e_split, r, a.d));
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-            const float4 s = f4_add(e[l + k * LPR], v[k]);
-            acc[l + k * LPR] = (a.mode == LGCN_EPI_INIT) ? s : f4_divmul(s, a.div, a.mul);
+            const float4 s = f4_add(ld_row(e + l + k * LPR, a.nt), v[k]);
+            st_row(acc + l + k * LPR, (a.mode == LGCN_EPI_INIT) ? s : f4_divmul(s, a.div, a.mul), a.nt);
         }
     } else if (a.mode == LGCN_EPI_STORE) {
 #pragma unroll
-        for (int k = 0; k < NV; ++k) acc[l + k * LPR] = v[k];
+        for (int k = 0; k < NV; ++k) st_row(acc + l + k * LPR, v[k], a.nt);
     } else if (a.mode == LGCN_EPI_SCALE) {
 #pragma unroll
         for (int k = 0; k < NV; ++k)
@@ -101,14 +119,14 @@ __device__ __forceinline__ void finish_row_vec(const SpmmArgs& a, int64_t r, int
     } else {
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-            const float4 s = f4_add(acc[l + k * LPR], v[k]);
-            acc[l + k * LPR] = (a.mode == LGCN_EPI_ADD) ? s : f4_divmul(s, a.div, a.mul);
+            const float4 s = f4_add(ld_row(acc + l + k * LPR, a.nt), v[k]);
+            st_row(acc + l + k * LPR, (a.mode == LGCN_EPI_ADD) ? s : f4_divmul(s, a.div, a.mul), a.nt);
         }
     }
     if (a.y != nullptr && (a.mode == LGCN_EPI_INIT || a.mode == LGCN_EPI_ADD)) {
         float4* y = reinterpret_cast<float4*>(a.y) + r * d4;
 #pragma unroll
-        for (int k = 0; k < NV; ++k) y[l + k * LPR] = v[k];
+        for (int k = 0; k < NV; ++k) st_row(y + l + k * LPR, v[k], a.nt);
     }
 }
 
@@ -330,7 +348,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
     if (SLICED && !(flags & kItemFirst)) {
         const float4* r = reinterpret_cast<const float4*>(a.run) + int64_t(it.dst) * d4 + l;
 #pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = r[k * LPR];
+        for (int k = 0; k < NV; ++k) acc[k] = ld_row(r + k * LPR, a.nt);
     } else {
 #pragma unroll
         for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -345,7 +363,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
     if (SLICED && !(flags & kItemLast)) {
         float4* r = reinterpret_cast<float4*>(a.run) + int64_t(it.dst) * d4 + l;
 #pragma unroll
-        for (int k = 0; k < NV; ++k) r[k * LPR] = acc[k];
+        for (int k = 0; k < NV; ++k) st_row(r + k * LPR, acc[k], a.nt);
         return;
     }
     finish_row_vec<LPR, NV>(a, it.dst, l, acc);
@@ -581,6 +599,12 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
     SpmmArgs a{items, n_items, splits, n_splits, col, val, x_lo, x_hi, x_split, e_lo, e_hi, e_split,
                y, acc_lo, acc_hi, acc_split, partial, d, mode, div, mul, run, chunks};
     hipStream_t s = as_stream(stream);
+    // Non-temporal row traffic (epilogue e/acc/y and running-sum loads and stores): those rows are
+    // touched once per launch, so they stream past the L2 and leave it to the gathered rows.
+    // Measured on C2 K=3 (profiles/r02z_nt/): d=64 1.274 -> 1.241 ms, d=32 0.747 -> 0.698. Off for
+    // block-split Cluster-GCN launches, whose y is the next layer's gathered table.
+    a.nt = (pass != PASS_BSPLIT) ? 3 : 0;
+    if (const char* nt = std::getenv("LGCN_SPMM_NT")) a.nt = std::atoi(nt);
 
     bool vec_ok = (d % 4 == 0) && aligned16(x_lo) && aligned16(acc_lo) && aligned16(partial) &&
                   (x_hi == nullptr || aligned16(x_hi)) && (acc_hi == nullptr || aligned16(acc_hi)) &&
