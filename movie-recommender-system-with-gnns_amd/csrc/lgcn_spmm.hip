@@ -601,9 +601,11 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
     hipStream_t s = as_stream(stream);
     // Non-temporal row traffic (epilogue e/acc/y and running-sum loads and stores): those rows are
     // touched once per launch, so they stream past the L2 and leave it to the gathered rows.
-    // Measured on C2 K=3 (profiles/r02z_nt/): d=64 1.274 -> 1.241 ms, d=32 0.747 -> 0.698. Off for
-    // block-split Cluster-GCN launches, whose y is the next layer's gathered table.
-    a.nt = (pass != PASS_BSPLIT) ? 3 : 0;
+    // Measured (profiles/r02z_nt/): sliced C2 K=3 d=64 1.274 -> 1.241 ms, d=32 0.747 -> 0.698. On
+    // for sliced launches and for tables beyond the Infinity Cache (C5); off for plain launches
+    // over cache-resident tables — the sharded ranks' plain schedule measured +2-3 % with it (their
+    // y is the next layer's gathered table) — and for block-split Cluster-GCN launches (+2.6 %).
+    a.nt = (pass != PASS_BSPLIT && (run != nullptr || N * int64_t(d) * 4 > (int64_t(512) << 20))) ? 3 : 0;
     if (const char* nt = std::getenv("LGCN_SPMM_NT")) a.nt = std::atoi(nt);
 
     bool vec_ok = (d % 4 == 0) && aligned16(x_lo) && aligned16(acc_lo) && aligned16(partial) &&
