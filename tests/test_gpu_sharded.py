@@ -70,7 +70,7 @@ def _reference(dev, case, R=1, F=1):
     return U, I, ei, uw, iw, np.concatenate(outs, axis=1), sched, F * sched.n_splits
 
 
-def _sharded(dev, case, world, rank, F=1):
+def _sharded(dev, case, world, rank, F=1, mode="allgather"):
     from lgcn_amd.sharded import BlockExchange, RowShards, ShardedPlan, ShardGrid, propagate_forward_sharded
 
     kind, K, d, chunk, slice_mb = CASES[case]
@@ -87,7 +87,7 @@ def _sharded(dev, case, world, rank, F=1):
     import torch.distributed as dist
 
     group = grid.exchange_group(dist) if world > 1 else None
-    ex = BlockExchange(shards, g_r, group) if grid.R > 1 else None
+    ex = BlockExchange(shards, g_r, group, grid.members, mode) if grid.R > 1 else None
     out = propagate_forward_sharded(x0p, splan, K, ex).cpu().numpy()
     a, b = shards.user_rows(g_r)
     c, e = shards.item_rows(g_r)
@@ -114,7 +114,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, case, out_dir, F=1):
+def _worker(rank, world, port, case, out_dir, F=1, mode="allgather"):
     import sys
 
     from conftest import PKG, ROOT
@@ -129,7 +129,7 @@ def _worker(rank, world, port, case, out_dir, F=1):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    shards, splan, ou, oi = _sharded(dev, case, world, rank, F)
+    shards, splan, ou, oi = _sharded(dev, case, world, rank, F, mode)
     g_r, c_g = rank // F, rank % F
     np.save(os.path.join(out_dir, f"u{g_r}_{c_g}.npy"), ou)
     np.save(os.path.join(out_dir, f"i{g_r}_{c_g}.npy"), oi)
@@ -139,9 +139,11 @@ def _worker(rank, world, port, case, out_dir, F=1):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,world,F", [(c, 2, 1) for c in CASES] + [("ml25m5_sliced", 2, 2), ("hub_sliced", 2, 2),
-                                                                     ("ml25m5_sliced", 4, 2), ("sub_K2_d128", 4, 2)])
-def test_sharded_ranks_bitwise(gpu, monkeypatch, tmp_path, case, world, F):
+@pytest.mark.parametrize("case,world,F,mode", [(c, 2, 1, "allgather") for c in CASES] +
+                         [("ml25m5_sliced", 2, 2, "allgather"), ("hub_sliced", 2, 2, "allgather"),
+                          ("ml25m5_sliced", 4, 2, "allgather"), ("sub_K2_d128", 4, 2, "allgather"),
+                          ("ml25m5_plain", 3, 1, "p2p"), ("hub_sliced", 4, 2, "p2p")])
+def test_sharded_ranks_bitwise(gpu, monkeypatch, tmp_path, case, world, F, mode):
     """world / F row groups x F column groups (gloo, every rank on the one GPU): the assembled
     output is bitwise the one-GPU forward with the schedule the ranks run (R = 1: each column share
     at its width; R > 1: lgcn_amd.sharded.rank_chunk at the full width); with R > 1 also within
@@ -152,7 +154,7 @@ def test_sharded_ranks_bitwise(gpu, monkeypatch, tmp_path, case, world, F):
     R = world // F
     U, I, ei, uw, iw, ref, sched, n_hubs = _reference(gpu, case, R, F)
     torch.cuda.synchronize()
-    mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path), F), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path), F, mode), nprocs=world, join=True)
     got_u = np.concatenate([np.concatenate([np.load(tmp_path / f"u{r}_{c}.npy") for c in range(F)], axis=1)
                             for r in range(R)])
     got_i = np.concatenate([np.concatenate([np.load(tmp_path / f"i{r}_{c}.npy") for c in range(F)], axis=1)
