@@ -66,6 +66,17 @@ __device__ __forceinline__ void adam_elem(float& p, float& g, float& m, float& v
     p = p + step_size * (m / denom);
 }
 
+// adam_elem with g == 0 (a missed step), the same floats with fewer instructions: g * coef and
+// g * g are +0, so v + omb2 * 0 == v * beta2 (v >= 0 and omb2 finite: adding +0 changes nothing),
+// and m + omb1 * (0 - m) == m - omb1 * m (0 - m == -m exactly for m != 0, m is never -0).
+__device__ __forceinline__ void adam_elem_zero(float& p, float& m, float& v, float step_size, float bc2_sqrt,
+                                               const AdamK& k) {
+    m = m - k.omb1 * m;
+    v = v * k.beta2;
+    const float denom = sqrtf(v) / bc2_sqrt + k.eps;
+    p = p + step_size * (m / denom);
+}
+
 __device__ __forceinline__ bool list_row(const RowList& L, int64_t i, int64_t& row) {
     if (i < L.n_a) {
         row = L.rows_a[i];
@@ -134,11 +145,10 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
         const float2 c = consts[s];
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
-            float z0 = 0.f, z1 = 0.f, z2 = 0.f, z3 = 0.f;
-            adam_elem(p[q].x, z0, m[q].x, v[q].x, 1.0f, c.x, c.y, k);
-            adam_elem(p[q].y, z1, m[q].y, v[q].y, 1.0f, c.x, c.y, k);
-            adam_elem(p[q].z, z2, m[q].z, v[q].z, 1.0f, c.x, c.y, k);
-            adam_elem(p[q].w, z3, m[q].w, v[q].w, 1.0f, c.x, c.y, k);
+            adam_elem_zero(p[q].x, m[q].x, v[q].x, c.x, c.y, k);
+            adam_elem_zero(p[q].y, m[q].y, v[q].y, c.x, c.y, k);
+            adam_elem_zero(p[q].z, m[q].z, v[q].z, c.x, c.y, k);
+            adam_elem_zero(p[q].w, m[q].w, v[q].w, c.x, c.y, k);
         }
     }
     int32_t now = static_cast<int32_t>(upto);
