@@ -211,8 +211,8 @@ def schedule_traffic(sched, n_src_rows: int, d: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", choices=["c2", "c5"], default="c2",
                     help="propagate workload: c2 = ML-25M-shaped K=3 d=64 (headline); c5 = 10M x 1M x 5e8, K=4 d=256")
     ap.add_argument("--layers", type=int, default=None, help="K (default 3 for c2, 4 for c5)")
