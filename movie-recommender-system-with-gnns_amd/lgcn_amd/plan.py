@@ -24,10 +24,14 @@ from . import _ffi
 
 DEFAULT_CHUNK = 256
 # hub chunk of the source-sliced schedule: a chunk is one lane group's sequential chain (one L2
-# latency per 8 edges), and every slice launch waits for its longest chain; 128 measured 2 %
-# faster than 256 on C2 and 1.4-1.6x faster on the small per-rank schedules of the sharded forward
-# (profiles/r02k_shard/)
-SLICED_CHUNK = 128
+# latency per 8 edges), and every slice launch waits for its longest chain, while shorter chunks
+# make more partials. Re-swept after the index rounds and non-temporal rows (profiles/r02zg/,
+# interleaved): C2 K=3 d=64 1.238 ms at 128, 1.225 at 160, 1.217 at 192, 1.235 at 224, 1.240 at
+# 256; d=32 within 1 % from 128 to 256.
+SLICED_CHUNK = 192
+# hub chunk of the plain schedule the sharded forward's ranks run when R > 1 (lgcn_amd.sharded.
+# rank_chunk): per-rank K=3 step at 8 x 1 0.246 ms at 128, 0.253 at 256 (profiles/r02k_shard/)
+RANK_CHUNK = 128
 
 
 def sliced_chunk(chunk: int) -> int:

@@ -146,11 +146,11 @@ class RowShards:
 
 def rank_chunk(chunk: int, R: int) -> int:
     """Hub chunk of a rank's schedule: the one-GPU chunk with one row group (same schedule as one
-    GPU, so bitwise its result); with R > 1 the plain schedule at min(chunk, SLICED_CHUNK) (a
+    GPU, so bitwise its result); with R > 1 the plain schedule at min(chunk, RANK_CHUNK) (a
     shorter longest chain per launch; per-rank K=3 step at 8x1: 0.253 ms at 256, 0.246 at 128)."""
-    from .plan import SLICED_CHUNK
+    from .plan import RANK_CHUNK
 
-    return int(chunk) if R == 1 else min(int(chunk), SLICED_CHUNK)
+    return int(chunk) if R == 1 else min(int(chunk), RANK_CHUNK)
 
 
 MIN_COLS = 32  # a column share narrower than 128 B rows stops cutting gather requests per edge

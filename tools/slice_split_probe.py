@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--layers", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=5)
     args = ap.parse_args()
     dev = torch.device("cuda")
     g = synth.ml25m_shaped(seed=0)
@@ -53,18 +54,26 @@ def main():
         return out, (time.perf_counter() - t) / args.steps * 1e3
 
     plan = PropagationPlan(ei, N, 256, side_split=U)
-    ref, ms0 = bench(lambda: lgcn_amd.propagate_forward(uw, iw, plan, K))
-    print(f"default      {ms0:.3f} ms/step  {K * E / ms0 / 1e6:.2f} e9 edges/s", flush=True)
+    runs = {"default": (None, lambda: lgcn_amd.propagate_forward(uw, iw, plan, K))}
+    ref = runs["default"][1]()
     for chunk in [int(c) for c in args.chunks.split(",")]:
         for cfg in args.cfg.split(","):
             ku, ki = (int(v) for v in cfg.split("x"))
             sd = build_sliced(plan.fwd, N, bounds_for(N, U, ku, ki), chunk)
-            torch.cuda.synchronize()
-            out, ms = bench(lambda: propagate_forward_sliced(uw, iw, sd, K))
-            rel = ((out - ref).abs().max(1).values / ref.abs().max(1).values.clamp_min(1e-30)).max().item()
-            print(f"ku={ku:2d} ki={ki:2d} chunk={chunk:4d}: {sd.n_launches:2d} launches, {sd.n_splits:5d} hub rows, "
-                  f"{ms:.3f} ms/step  {K * E / ms / 1e6:.2f} e9 edges/s  max row-rel diff {rel:.2e}", flush=True)
-            del sd
+            runs[f"ku={ku:2d} ki={ki:2d} chunk={chunk:4d}"] = (sd, lambda s=sd: propagate_forward_sliced(uw, iw, s, K))
+    # interleaved rounds: every configuration timed once per round, medians reported
+    times = {n: [] for n in runs}
+    for _ in range(args.rounds):
+        for n, (_, fn) in runs.items():
+            times[n].append(bench(fn)[1])
+    for n, (sd, fn) in runs.items():
+        out = fn()
+        rel = ((out - ref).abs().max(1).values / ref.abs().max(1).values.clamp_min(1e-30)).max().item()
+        t = sorted(times[n])
+        ms = t[len(t) // 2]
+        desc = f"{sd.n_launches:2d} launches, {sd.n_splits:5d} hub rows, " if sd is not None else ""
+        print(f"{n}: {desc}{ms:.3f} ms/step  {K * E / ms / 1e6:.2f} e9 edges/s  max row-rel diff {rel:.2e}",
+              flush=True)
 
 
 if __name__ == "__main__":
