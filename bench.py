@@ -252,7 +252,7 @@ def main():
 
     import lgcn_amd
     from lgcn_amd import synth
-    from lgcn_amd.plan import DEFAULT_CHUNK, PropagationPlan
+    from lgcn_amd.plan import DEFAULT_CHUNK, PropagationPlan, sliced_chunk
     from lgcn_amd.sliced import SlicedDirection
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -471,6 +471,8 @@ def main():
                      "effective_GBps": alg_launch / (kernel_ms * 1e-3) / 1e9},
         "cpu_baseline": None,
     }
+    if sliced:
+        result["config"]["hub_chunk_sliced"] = sliced_chunk(chunk)  # the source-sliced schedule's hub chunk
     if grid_trials is not None:
         result["config"]["grid_trials_ms_per_step"] = grid_trials
     if exchange is not None:
