@@ -270,7 +270,12 @@ int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split,
                    const int64_t* u, const int64_t* p, const int64_t* n, int64_t B, int32_t d,
                    const uint8_t* touched, float div, float mul,
                    float coeff, float* cf, float* cw, float* terms, lgcn_stream_t stream);
-int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* loss, lgcn_stream_t stream);
+/* partial: NULL, or float[2 * LGCN_LOSS_PARTS] scratch — large batches then sum in two stages
+ * (LGCN_LOSS_PARTS blocks over contiguous shares, one block over the shares): a fixed association
+ * either way, so the loss is deterministic. */
+#define LGCN_LOSS_PARTS 256
+int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* loss, float* partial,
+                  lgcn_stream_t stream);
 int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C, int64_t N, int32_t d,
                       float* out_lo, float* out_hi, int64_t split, int32_t add, float mul, float div,
                       lgcn_stream_t stream);

@@ -10,7 +10,7 @@
 //                 cosines, layer-0 W rows for the reg term), reduces the 6 dot products inside
 //                 the group, and writes the per-triplet gradient rows (dF for u, p, n and the
 //                 reg gradient for W) plus the two loss terms — no atomics;
-//   k_bpr_loss    deterministic single-block sum of the loss terms;
+//   k_bpr_loss    deterministic sum of the loss terms (one block, or 256 shares + one block);
 //   k_segment_rows  adds the gradient rows into their destination rows in a fixed (stable
 //                 sorted) order using the CSR lgcn_csr_build makes of the 3B row keys.
 // The gradient is the analytic derivative of the same expression (not bitwise torch autograd).
@@ -182,21 +182,22 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
 }
 
 constexpr int kLossBlock = 1024;
+constexpr int kLossPartBlock = 256;
 
-__global__ __launch_bounds__(kLossBlock) void k_bpr_loss(const float* __restrict__ terms, int64_t B, int32_t d,
-                                                         float coeff, float* __restrict__ loss) {
+// Sums of t[0..n) and t[stride..stride+n) by one block (each thread its strided terms in index
+// order, loads issued 8 at a time, then the fixed wave/LDS tree), into the loss of B triplets.
+__global__ __launch_bounds__(kLossBlock) void k_bpr_loss(const float* __restrict__ t, int64_t n, int64_t stride,
+                                                         int64_t B, int32_t d, float coeff, float* __restrict__ loss) {
     __shared__ float r0[kLossBlock / 64], r1[kLossBlock / 64];
     float s0 = 0.f, s1 = 0.f;
-    // each thread sums its strided terms in index order; loads are issued 8 at a time (one
-    // memory latency per 8 terms instead of one per term — same additions, same result)
     constexpr int kU = 8;
     int64_t i = threadIdx.x;
-    for (; i + (kU - 1) * int64_t(kLossBlock) < B; i += kU * int64_t(kLossBlock)) {
+    for (; i + (kU - 1) * int64_t(kLossBlock) < n; i += kU * int64_t(kLossBlock)) {
         float a[kU], c[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            a[u] = terms[i + u * int64_t(kLossBlock)];
-            c[u] = terms[B + i + u * int64_t(kLossBlock)];
+            a[u] = t[i + u * int64_t(kLossBlock)];
+            c[u] = t[stride + i + u * int64_t(kLossBlock)];
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -204,9 +205,9 @@ __global__ __launch_bounds__(kLossBlock) void k_bpr_loss(const float* __restrict
             s1 += c[u];
         }
     }
-    for (; i < B; i += kLossBlock) {
-        s0 += terms[i];
-        s1 += terms[B + i];
+    for (; i < n; i += kLossBlock) {
+        s0 += t[i];
+        s1 += t[stride + i];
     }
     for (int off = 32; off > 0; off >>= 1) {
         s0 += __shfl_down(s0, off, 64);
@@ -226,6 +227,55 @@ __global__ __launch_bounds__(kLossBlock) void k_bpr_loss(const float* __restrict
         const float bf = static_cast<float>(B);
         // -(mean softplus) / 10 + coeff * mean(squares); B == 0 gives NaN, as torch's empty mean
         loss[0] = -((a / bf) / 10.0f) + coeff * (c / (bf * static_cast<float>(d)));
+    }
+}
+
+// First stage of the two-stage sum: block p sums its contiguous share of each term array (threads
+// strided in index order, then the fixed wave/LDS tree) into part[p] and part[P + p].
+__global__ __launch_bounds__(kLossPartBlock) void k_bpr_loss_part(const float* __restrict__ terms, int64_t B,
+                                                                  float* __restrict__ part) {
+    __shared__ float r0[kLossPartBlock / 64], r1[kLossPartBlock / 64];
+    const int64_t P = gridDim.x;
+    const int64_t per = (B + P - 1) / P;
+    const int64_t lo = int64_t(blockIdx.x) * per;
+    const int64_t hi = lo + per < B ? lo + per : B;
+    float s0 = 0.f, s1 = 0.f;
+    constexpr int kU = 4;
+    int64_t i = lo + threadIdx.x;
+    for (; i + (kU - 1) * int64_t(kLossPartBlock) < hi; i += kU * int64_t(kLossPartBlock)) {
+        float a[kU], c[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            a[u] = terms[i + u * int64_t(kLossPartBlock)];
+            c[u] = terms[B + i + u * int64_t(kLossPartBlock)];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            s0 += a[u];
+            s1 += c[u];
+        }
+    }
+    for (; i < hi; i += kLossPartBlock) {
+        s0 += terms[i];
+        s1 += terms[B + i];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        s0 += __shfl_down(s0, off, 64);
+        s1 += __shfl_down(s1, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        r0[threadIdx.x >> 6] = s0;
+        r1[threadIdx.x >> 6] = s1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float a = 0.f, c = 0.f;
+        for (int w = 0; w < kLossPartBlock / 64; ++w) {
+            a += r0[w];
+            c += r1[w];
+        }
+        part[blockIdx.x] = a;
+        part[P + blockIdx.x] = c;
     }
 }
 
@@ -738,9 +788,19 @@ int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, co
 #undef LGCN_FRA
 }
 
-int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* loss, lgcn_stream_t stream) {
+int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* loss, float* partial,
+                  lgcn_stream_t stream) {
     if (B < 0 || !loss || (B > 0 && !terms)) return fail(LGCN_E_ARG, "lgcn_bpr_loss: bad args");
-    k_bpr_loss<<<1, kLossBlock, 0, as_stream(stream)>>>(terms, B, d, coeff, loss);
+    hipStream_t s = as_stream(stream);
+    // large batches: LGCN_LOSS_PARTS blocks sum contiguous shares, one block sums the shares
+    // (a single block over 2B terms is latency-bound: 26 us at B = 180k)
+    if (partial != nullptr && B >= 16 * int64_t(LGCN_LOSS_PARTS) * kLossPartBlock / 64) {
+        k_bpr_loss_part<<<LGCN_LOSS_PARTS, kLossPartBlock, 0, s>>>(terms, B, partial);
+        if (int rc = check_launch("k_bpr_loss_part")) return rc;
+        k_bpr_loss<<<1, kLossBlock, 0, s>>>(partial, LGCN_LOSS_PARTS, LGCN_LOSS_PARTS, B, d, coeff, loss);
+        return check_launch("k_bpr_loss");
+    }
+    k_bpr_loss<<<1, kLossBlock, 0, s>>>(terms, B, B, B, d, coeff, loss);
     return check_launch("k_bpr_loss");
 }
 

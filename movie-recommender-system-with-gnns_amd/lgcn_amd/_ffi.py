@@ -27,6 +27,7 @@ ABI_VERSION = 2  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
 
 _lib = None
 
+LOSS_PARTS = 256  # include/lgcn.h LGCN_LOSS_PARTS
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
 _i32 = ctypes.c_int32
@@ -65,7 +66,7 @@ _SIGS = {
     "lgcn_bpr_fused": ([_vp, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _f32, _f32, _f32, _vp, _vp,
                         _vp, _vp],
                        ctypes.c_int),
-    "lgcn_bpr_loss": ([_vp, _i64, _i32, _f32, _vp, _vp], ctypes.c_int),
+    "lgcn_bpr_loss": ([_vp, _i64, _i32, _f32, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_segment_rows": ([_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _i32, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_range_scatter_add": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _i64,
                                 _f32, _i64, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),

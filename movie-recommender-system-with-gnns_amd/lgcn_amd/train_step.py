@@ -93,6 +93,7 @@ class _BatchState:
         self.cw = None if self.small else torch.empty((3 * B, d), dtype=torch.float32, device=dev)
         self.terms = torch.empty(2 * B, dtype=torch.float32, device=dev)
         self.loss = torch.empty(1, dtype=torch.float32, device=dev)
+        self.loss_part = torch.empty(2 * _ffi.LOSS_PARTS, dtype=torch.float32, device=dev)
         self.rowptr = torch.empty(N + 1, dtype=torch.int64, device=dev)
         self.col = torch.empty(3 * B, dtype=torch.int32, device=dev)
         self.eid = torch.empty(3 * B, dtype=torch.int32, device=dev)
@@ -211,7 +212,8 @@ class FusedTrainStep:
                                           st.plan.touched.data_ptr(), div, mul,
                                           self.coeff, st.cf.data_ptr(), _ffi.ptr(st.cw), st.terms.data_ptr(),
                                           stream), "lgcn_bpr_fused")
-            _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(), stream),
+            _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(),
+                                         st.loss_part.data_ptr(), stream),
                        "lgcn_bpr_loss")
             gu = torch.empty((U, d), dtype=torch.float32, device=dev)
             gi = torch.empty((I, d), dtype=torch.float32, device=dev)
@@ -278,7 +280,8 @@ class FusedTrainStep:
                                           st.plan.touched.data_ptr(), div, mul,
                                           self.coeff, st.cf.data_ptr(), _ffi.ptr(st.cw), st.terms.data_ptr(),
                                           stream), "lgcn_bpr_fused")
-            _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(), stream),
+            _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(),
+                                         st.loss_part.data_ptr(), stream),
                        "lgcn_bpr_loss")
             gu, gi = opt.gu, opt.gi
             grads = (gu, gi, U)
