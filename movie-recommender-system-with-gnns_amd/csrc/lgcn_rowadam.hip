@@ -228,7 +228,7 @@ __global__ void k_step_advance(int64_t* step) {
     if (threadIdx.x == 0 && blockIdx.x == 0) step[0] += 1;
 }
 
-constexpr int kRowNormBlocks = 512;
+constexpr int kRowNormBlocks = 2048;
 
 template <int LPR, int NV>
 int launch_row_adam(const RowTables& T, const RowList& L, int64_t n_rows, int32_t* last, int32_t* claim,
