@@ -8,7 +8,7 @@ OUT=$R/gpurun_out/${PROF_TAG:-prof_round}
 mkdir -p "$OUT"
 cd "$R"
 P="timeout -k 10 300 rocprofv3"
-$P --kernel-trace --stats -T -d "$OUT/trace" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 > "$OUT/trace.log" 2>&1
+$P --kernel-trace --stats -T -d "$OUT/trace" -o run --output-format csv -- python3 bench.py > "$OUT/trace.log" 2>&1
 $P --pmc FETCH_SIZE -T -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1
 $P --pmc WRITE_SIZE -T -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1
 $P --pmc FETCH_SIZE -T -d "$OUT/calib_fetch" -o run --output-format csv -- python3 tools/calib_fetch.py > "$OUT/calib_fetch.log" 2>&1
