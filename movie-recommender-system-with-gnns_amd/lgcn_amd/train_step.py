@@ -206,7 +206,8 @@ class FusedTrainStep:
         with torch.no_grad():
             out = propagate_forward(uw.detach(), iw.detach(), st.plan, K)
             torch.randint(0, I, (B,), device=dev, out=st.neg)
-            torch.add(st.neg, U, out=st.keys[2 * B:])
+            if not st.small:  # only the all-keys sort reads the negatives' global row keys
+                torch.add(st.neg, U, out=st.keys[2 * B:])
             _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
                                           st.users.data_ptr(), st.pos.data_ptr(), st.neg.data_ptr(), B, d,
                                           st.plan.touched.data_ptr(), div, mul,
@@ -272,7 +273,6 @@ class FusedTrainStep:
         big = 1 << 62
         with torch.no_grad():
             torch.randint(0, I, (B,), device=dev, out=st.neg)
-            torch.add(st.neg, U, out=st.keys[2 * B:])
             opt.catch_up(st.touched_rows, st.neg, U)
             out = propagate_forward(uw.detach(), iw.detach(), st.plan, K)
             _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
