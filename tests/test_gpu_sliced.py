@@ -147,3 +147,27 @@ def test_uncoalesced_edges_fall_back_to_plain_schedule(gpu, force_slices):
     assert_rows_close(out, np.concatenate([ru, ri]))
 
 
+
+
+@pytest.mark.parametrize("d,cms", [(64, ["1", "2", "4"]), (32, ["1", "4", "8"]), (16, ["2", "8", "16"]),
+                                   (8, ["4", "16", "32"])])
+@pytest.mark.parametrize("sliced", [True, False])
+def test_index_rounds_bitwise(gpu, force_slices, monkeypatch, d, cms, sliced):
+    """Index load rounds (LGCN_SPMM_CM batches of col/val per load round) only change how many
+    indices a lane group loads at once, never the adds: every round size gives the same floats,
+    on the sliced and the plain schedule, and matches the oracle."""
+    from lgcn_amd.propagate import lgconv_forward
+
+    U, I, ei = graphs.hub(U=900, I=80)
+    N = U + I
+    force_slices(0.004 if sliced else 0)
+    plan = _plan(ei, N, gpu, U, chunk=24)
+    x = torch.from_numpy(np.random.default_rng(d).standard_normal((N, d)).astype(np.float32)).to(gpu)
+    outs = []
+    for cm in cms:
+        monkeypatch.setenv("LGCN_SPMM_CM", cm)
+        outs.append(lgconv_forward(x, plan).cpu().numpy())
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+    _, w = c_oracle.gcn_norm(ei, N)
+    assert_rows_close(outs[0], c_oracle.lgconv(x.cpu().numpy(), ei, w))
