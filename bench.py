@@ -576,7 +576,8 @@ def run_train(args):
         # row-sparse DP gradient exchange: all_gather of each rank's nonzero gradient rows
         cap = D.exchange_capacity(batches, U)
         exchange = D.RowExchange(cap, N, d, dev, world)
-        log(f"[rank {rank}] row exchange: {cap} slots per rank, {cap * (4 * d + 8) / 1e6:.1f} MB sent per step "
+        log(f"[rank {rank}] row exchange: {exchange.cap} slots per rank, one all_gather of "
+            f"{exchange.blk * 4 / 1e6:.1f} MB per rank per step "
             f"(dense all_reduce: {N * d * 4 / 1e6:.1f} MB)")
     if not args.autograd:
         from lgcn_amd.train_step import FusedTrainStep
@@ -643,7 +644,7 @@ def run_train(args):
                    "parts_per_batch": q, "f_intra": f_intra, "layers": K, "dim": d, "num_users": U,
                    "num_items": I, "train_edges": n_tr,
                    "parallelism": (f"dp{world}: disjoint part batches per rank, " +
-                                   ("row-sparse gradient exchange (all_gather of each rank's nonzero rows), "
+                                   ("row-sparse gradient exchange (one all_gather per step of each rank's nonzero rows and their ids), "
                                     "row-lazy Adam on the union" if exchange is not None else
                                     "RCCL all_reduce of embedding grads" if world > 1 else "single GPU"))},
     }

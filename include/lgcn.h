@@ -424,13 +424,16 @@ int lgcn_adam_prologue(double* step, float lr, double beta1, double beta2, float
  *   lgcn_rows_mark_first: first[i] = 1 iff ids[i] >= 0 is the lowest index holding that row;
  *     claim int32[N] must hold INT32_MAX on entry and holds it again on exit.
  *   lgcn_rows_accumulate: for r = 0..world-1 in order, over slots [r*cap, (r+1)*cap):
- *     g[row] = first ? rows[i] : g[row] + rows[i]; then, if div > 0, g[row] /= div once per row. */
+ *     g[row] = first ? rows[i] : g[row] + rows[i]; then, if div > 0, g[row] /= div once per row.
+ *     Rank r's rows start at rows + r*rank_stride (floats; >= cap*d, a multiple of 4): cap*d for
+ *     separate row tables, cap*(d+2) for the one-collective records [ids as 2*cap floats | rows]. */
 int lgcn_rows_pack(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
                    int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
                    const uint8_t* skip_b, int64_t cap, int64_t* ids, float* rows, lgcn_stream_t stream);
 int lgcn_rows_mark_first(const int64_t* ids, int64_t n, int32_t* claim, uint8_t* first, lgcn_stream_t stream);
-int lgcn_rows_accumulate(const int64_t* ids, const float* rows, int64_t world, int64_t cap, const uint8_t* first,
-                         float* g_lo, float* g_hi, int64_t split, int32_t d, float div, lgcn_stream_t stream);
+int lgcn_rows_accumulate(const int64_t* ids, const float* rows, int64_t world, int64_t cap, int64_t rank_stride,
+                         const uint8_t* first, float* g_lo, float* g_hi, int64_t split, int32_t d, float div,
+                         lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Host-side (no GPU): balanced k-way node partition for Cluster-GCN batching, the METIS

@@ -171,19 +171,19 @@ int lgcn_rows_mark_first(const int64_t* ids, int64_t n, int32_t* claim, uint8_t*
     return check_launch("k_claim_reset");
 }
 
-int lgcn_rows_accumulate(const int64_t* ids, const float* rows, int64_t world, int64_t cap, const uint8_t* first,
-                         float* g_lo, float* g_hi, int64_t split, int32_t d, float div, lgcn_stream_t stream) {
-    if (world < 1 || cap < 0 || !g_lo || (cap > 0 && (!ids || !rows || !first)))
-        return fail(LGCN_E_ARG, "lgcn_rows_accumulate: bad args");
-    if (!al16(g_lo) || (g_hi && !al16(g_hi)) || (rows && !al16(rows)))
-        return fail(LGCN_E_UNSUPPORTED, "lgcn_rows_accumulate: tables must be 16-byte aligned");
+int lgcn_rows_accumulate(const int64_t* ids, const float* rows, int64_t world, int64_t cap, int64_t rank_stride,
+                         const uint8_t* first, float* g_lo, float* g_hi, int64_t split, int32_t d, float div,
+                         lgcn_stream_t stream) {
+    if (world < 1 || cap < 0 || !g_lo || (cap > 0 && (!ids || !rows || !first)) || rank_stride < cap * int64_t(d))
+        return fail(LGCN_E_ARG, "lgcn_rows_accumulate: bad args (rank_stride=%lld < cap*d?)", (long long)rank_stride);
+    if (!al16(g_lo) || (g_hi && !al16(g_hi)) || (rows && !al16(rows)) || rank_stride % 4)
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_rows_accumulate: tables and rank blocks must be 16-byte aligned");
     if (cap == 0) return LGCN_OK;
     hipStream_t s = as_stream(stream);
-    const int64_t dd = d;
 #define LGCN_AC(LP, NVV)                                                                                         \
     for (int64_t r = 0; r < world; ++r) {                                                                        \
         k_rows_accumulate<LP, NVV><<<grid_for(cap * LP, kBlock, int64_t(1) << 30), kBlock, 0, s>>>(                \
-            ids + r * cap, rows + r * cap * dd, cap, first + r * cap, g_lo, g_hi, split, d, 0, 1.0f);            \
+            ids + r * cap, rows + r * rank_stride, cap, first + r * cap, g_lo, g_hi, split, d, 0, 1.0f);            \
         if (int rc = check_launch("k_rows_accumulate")) return rc;                                               \
     }                                                                                                            \
     if (div > 0.f)                                                                                               \

@@ -82,7 +82,7 @@ _SIGS = {
     "lgcn_rows_pack": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
                        ctypes.c_int),
     "lgcn_rows_mark_first": ([_vp, _i64, _vp, _vp, _vp], ctypes.c_int),
-    "lgcn_rows_accumulate": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _f32, _vp], ctypes.c_int),
+    "lgcn_rows_accumulate": ([_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _f32, _vp], ctypes.c_int),
     "lgcn_recall_width": ([_i32, _vp, _vp], ctypes.c_int),
     "lgcn_normalize_rows": ([_vp, _vp, _i64, _i64, _i32, _vp, _i32, _i64, _vp], ctypes.c_int),
     "lgcn_score_filter": ([_vp, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp], ctypes.c_int),

@@ -74,33 +74,45 @@ def exchange_capacity(batches, num_users: int) -> int:
 class RowExchange:
     """Row-sparse DP gradient exchange for the row-lazy optimizer (csrc/lgcn_exchange.hip).
 
-    Per step each rank packs its listed gradient rows (ids int64 [cap], rows [cap, d]); the
-    packs are all-gathered (RCCL over xGMI; gloo in tests) and every rank sums them per row in
-    rank order and divides by W, so the union's gradient rows — and the clip norm and Adam update
-    over them — are bitwise identical on every rank. Bytes per rank per step: cap * (4d + 8),
-    against 4d * N for the dense all_reduce (C4: ~17k rows of 512 B vs 113 MB)."""
+    Per step each rank packs its listed gradient rows into ONE record block (fp32 [cap*(d+2)]:
+    the slot ids as int64 [cap] in the first 2*cap words, then the rows [cap, d]); the blocks are
+    all-gathered in one collective (RCCL over xGMI; gloo in tests), the ids copied out contiguous,
+    and every rank sums the rows per row in rank order and divides by W, so the union's gradient
+    rows — and the clip norm and Adam update over them — are bitwise identical on every rank.
+    Bytes per rank per step: cap * (4d + 8), against 4d * N for the dense all_reduce (C4: ~17k
+    rows of 512 B vs 113 MB)."""
 
     def __init__(self, cap: int, N: int, d: int, device, world: int):
-        self.cap, self.N, self.d, self.world = int(cap), int(N), int(d), int(world)
-        self.ids = torch.full((self.cap,), -1, dtype=torch.int64, device=device)
-        self.rows = torch.zeros((self.cap, self.d), dtype=torch.float32, device=device)
+        # cap even: each rank's block (cap*(d+2) words) and its rows (after 2*cap words) stay
+        # 16-byte aligned for the float4 kernels (d % 4 == 0)
+        self.cap, self.N, self.d, self.world = int(cap) + int(cap) % 2, int(N), int(d), int(world)
+        self.blk = self.cap * (self.d + 2)
+        self.pack = torch.zeros(self.blk, dtype=torch.float32, device=device)
+        self.ids = self.pack[:2 * self.cap].view(torch.int64)
+        self.ids.fill_(-1)
+        self.rows = self.pack[2 * self.cap:].view(self.cap, self.d)
+        self.pack_all = torch.zeros(self.world * self.blk, dtype=torch.float32, device=device)
         self.ids_all = torch.full((self.world * self.cap,), -1, dtype=torch.int64, device=device)
-        self.rows_all = torch.zeros((self.world * self.cap, self.d), dtype=torch.float32, device=device)
         self.first = torch.zeros(self.world * self.cap, dtype=torch.uint8, device=device)
         self.claim = torch.full((self.N,), 2**31 - 1, dtype=torch.int32, device=device)
 
+    def rows_ptr(self) -> int:
+        """device pointer of rank 0's rows in the gathered records."""
+        return self.pack_all.data_ptr() + 8 * self.cap
+
+    def unpack_ids(self) -> None:
+        """ids_all[r*cap + j] = rank r's slot j id (captured with the step's second half)."""
+        blocks = self.pack_all.view(self.world, self.blk)[:, :2 * self.cap].view(torch.int64)
+        self.ids_all.view(self.world, self.cap).copy_(blocks)
+
     def gather(self) -> None:
-        """The collective (eager, between the step's two captured halves)."""
+        """The collective (eager, between the step's two captured halves): one per step."""
         if self.world == 1:
-            self.ids_all.copy_(self.ids)
-            self.rows_all.copy_(self.rows)
-            return
-        if dist.get_backend() == "nccl":
-            dist.all_gather_into_tensor(self.ids_all, self.ids)
-            dist.all_gather_into_tensor(self.rows_all, self.rows)
+            self.pack_all.copy_(self.pack)
+        elif dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(self.pack_all, self.pack)
         else:
-            dist.all_gather(list(self.ids_all.view(self.world, self.cap).unbind(0)), self.ids)
-            dist.all_gather(list(self.rows_all.view(self.world, self.cap, self.d).unbind(0)), self.rows)
+            dist.all_gather(list(self.pack_all.view(self.world, self.blk).unbind(0)), self.pack)
 
 
 def train_epoch(model, optimizer, batches, device, seed: int = 0, epoch: int = 0, loss_fn=None,

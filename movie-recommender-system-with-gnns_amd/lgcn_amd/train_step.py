@@ -319,9 +319,10 @@ class FusedTrainStep:
             m = self.model
             stream = _ffi.stream_of(ex.ids_all.device)
             n = ex.world * ex.cap
+            ex.unpack_ids()
             _ffi.check(lib.lgcn_rows_mark_first(ex.ids_all.data_ptr(), n, ex.claim.data_ptr(), ex.first.data_ptr(),
                                                 stream), "lgcn_rows_mark_first")
-            _ffi.check(lib.lgcn_rows_accumulate(ex.ids_all.data_ptr(), ex.rows_all.data_ptr(), ex.world, ex.cap,
+            _ffi.check(lib.lgcn_rows_accumulate(ex.ids_all.data_ptr(), ex.rows_ptr(), ex.world, ex.cap, ex.blk,
                                                 ex.first.data_ptr(), opt.gu.data_ptr(), opt.gi.data_ptr(),
                                                 m.num_users, m.dim_h, float(ex.world), stream),
                        "lgcn_rows_accumulate")

@@ -35,10 +35,13 @@ def _pack(lib, g, U, d, rows_a, keys_b, first_b, skip_b, cap, gpu):
     return ids, rows
 
 
+@pytest.mark.parametrize("records", [False, True])
 @pytest.mark.parametrize("d", [64, 128])
-def test_exchange_kernels_match_sequential_restatement(gpu, d):
+def test_exchange_kernels_match_sequential_restatement(gpu, d, records):
     """pack (3 ranks' lists with duplicates, filters, padding) -> mark_first -> accumulate(/3),
-    bitwise against: for each slot in rank order, first occurrence stores, later ones add, /3."""
+    bitwise against: for each slot in rank order, first occurrence stores, later ones add, /3.
+    records: the rows read from RowExchange's one-collective layout (rank blocks of
+    [ids as 2*cap words | rows], rank_stride = cap*(d+2)) instead of one dense row table."""
     from lgcn_amd import _ffi
 
     lib = _ffi.load()
@@ -74,7 +77,15 @@ def test_exchange_kernels_match_sequential_restatement(gpu, d):
     _ffi.check(lib.lgcn_rows_mark_first(ids_all.data_ptr(), W * cap, claim.data_ptr(), first.data_ptr(), s), "mf")
     assert torch.equal(claim, torch.full_like(claim, 2**31 - 1))
     g = torch.full((N, d), float("nan"), device=gpu)  # rows outside the union must stay untouched
-    _ffi.check(lib.lgcn_rows_accumulate(ids_all.data_ptr(), rows_all.data_ptr(), W, cap, first.data_ptr(),
+    if records:
+        blk = cap * (d + 2)
+        rec = torch.full((W, blk), float("nan"), device=gpu)
+        rec[:, :2 * cap] = ids_all.view(W, cap).view(torch.float32)
+        rec[:, 2 * cap:] = rows_all.view(W, cap * d)
+        rows_ptr, stride = rec.data_ptr() + 8 * cap, blk
+    else:
+        rows_ptr, stride = rows_all.data_ptr(), cap * d
+    _ffi.check(lib.lgcn_rows_accumulate(ids_all.data_ptr(), rows_ptr, W, cap, stride, first.data_ptr(),
                                         g[:U].data_ptr(), g[U:].data_ptr(), U, d, float(W), s), "acc")
     ids_h = ids_all.cpu().numpy()
     rows_h = rows_all.cpu()
