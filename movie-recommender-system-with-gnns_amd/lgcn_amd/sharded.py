@@ -169,9 +169,12 @@ def grid_shape(world: int, d: int) -> tuple[int, int]:
 
 def grid_candidates(world: int, d: int) -> list[tuple[int, int, str | None]]:
     """(R, F, exchange mode) grids bench.py times before it picks one for a world of ranks: every
-    column split F | world with d / F a multiple of 4 and >= 8, rows-only grids (F = 1) only when
-    no column split exists (they move the most bytes), both exchange modes where a row group has
-    three or more ranks (an all_gather and direct peer sends differ there), none with R = 1."""
+    column split F | world with d / F a multiple of 4 and >= 8; the rows-only grid (F = 1) when no
+    column split exists or when world >= 4 — it moves the most bytes in total, but over R - 1 links
+    at once, so its bytes per xGMI link match the column-split grids' (C2 at N = 8: ~14 MB per link
+    per step for 8 x 1, 4 x 2 and 2 x 4) at the least compute per rank; both exchange modes where a
+    row group has three or more ranks (an all_gather and direct peer sends differ there), none with
+    R = 1."""
     out = []
     for F in range(world, 0, -1):
         if world % F or d % F or (d // F) % 4 or d // F < 8:
@@ -181,7 +184,7 @@ def grid_candidates(world: int, d: int) -> list[tuple[int, int, str | None]]:
             out.append((R, F, None))
         else:
             out += [(R, F, m) for m in (EXCHANGE_MODES if R >= 3 else EXCHANGE_MODES[:1])]
-    if any(F > 1 for _, F, _ in out):
+    if any(F > 1 for _, F, _ in out) and world < 4:
         out = [c for c in out if c[1] > 1]
     return out
 

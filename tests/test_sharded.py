@@ -200,9 +200,10 @@ def test_grid_candidates():
 
     assert grid_candidates(1, 64) == [(1, 1, None)]
     assert grid_candidates(2, 64) == [(1, 2, None)]
-    assert grid_candidates(4, 64) == [(1, 4, None), (2, 2, "allgather")]
-    assert grid_candidates(8, 64) == [(1, 8, None), (2, 4, "allgather"), (4, 2, "allgather"), (4, 2, "p2p")]
-    assert grid_candidates(3, 64) == [(3, 1, "allgather"), (3, 1, "p2p")]   # odd world: rows only
-    assert grid_candidates(8, 32) == [(2, 4, "allgather"), (4, 2, "allgather"), (4, 2, "p2p")]  # 4-col shares: no
+    rows_only = lambda w: [(w, 1, "allgather"), (w, 1, "p2p")]  # noqa: E731 (world >= 4: R - 1 >= 3 links)
+    assert grid_candidates(4, 64) == [(1, 4, None), (2, 2, "allgather")] + rows_only(4)
+    assert grid_candidates(8, 64) == [(1, 8, None), (2, 4, "allgather"), (4, 2, "allgather"), (4, 2, "p2p")] + rows_only(8)
+    assert grid_candidates(3, 64) == rows_only(3)   # odd world: rows only
+    assert grid_candidates(8, 32) == [(2, 4, "allgather"), (4, 2, "allgather"), (4, 2, "p2p")] + rows_only(8)  # 4-col shares: no
     for R, F, _ in grid_candidates(8, 256):
         assert R * F == 8 and (256 // F) % 4 == 0
