@@ -1,4 +1,4 @@
-"""Row-sharded propagation (lgcn_amd.sharded), host logic on CPU, world_size 2 and 3 on gloo.
+"""Row-sharded propagation (lgcn_amd.sharded), host logic on CPU, world_size 2, 3, 4 and 8 on gloo.
 
 The HIP kernels need a GPU, so each rank's "kernel" here is a CPU stand-in (CpuShardPlan) that
 computes a layer with the oracle restatement (oracle/lgconv_ref.py) and keeps only the rows the
@@ -120,7 +120,8 @@ def _worker(rank, world, port, kind, K, out_dir, F=1, mode="allgather"):
                                                  ("nonbip", 2, 3, 1, "allgather"), ("sub", 2, 1, 1, "allgather"),
                                                  ("sub", 2, 3, 2, "allgather"), ("hub", 4, 3, 2, "allgather"),
                                                  ("nonbip", 4, 2, 2, "allgather"), ("sym", 3, 2, 1, "p2p"),
-                                                 ("hub", 4, 3, 2, "p2p"), ("sub", 4, 3, 1, "p2p")])
+                                                 ("hub", 4, 3, 2, "p2p"), ("sub", 4, 3, 1, "p2p"),
+                                                 ("hub", 8, 3, 1, "p2p")])
 def test_sharded_equals_single_rank_bitwise(tmp_path, kind, world, K, F, mode):
     """R = world / F row groups x F column groups (F = 2: each rank propagates 8 of the 16
     columns; ranks of one column group exchange rows, column groups exchange nothing); the rows
