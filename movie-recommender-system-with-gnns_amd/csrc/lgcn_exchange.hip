@@ -5,12 +5,15 @@
 // % of N, so each rank ships just those rows:
 //
 //   lgcn_rows_pack        rank r: its listed rows -> ids[cap] (int64, -1 = empty) + rows[cap, d]
-//   (all_gather over RCCL of ids and rows: [W, cap] and [W, cap, d])
+//                         (lgcn_amd.distributed.RowExchange packs both into one record block:
+//                         the ids as the first 2*cap words, then the rows)
+//   (one all_gather over RCCL of the record blocks: [W, cap*(d+2)]; ids copied out contiguous)
 //   lgcn_rows_mark_first  first[i] = entry i is the first occurrence of its row in the gathered
 //                         list (deterministic: lowest index wins; claim[N] int32 = INT32_MAX
 //                         between calls, restored on exit)
-//   lgcn_rows_accumulate  per rank r = 0..W-1 in order: g[row] = first ? row_r : g[row] + row_r;
-//                         then g[row] /= W on the first entries (div > 0)
+//   lgcn_rows_accumulate  per rank r = 0..W-1 in order (rank r's rows at rows + r*rank_stride):
+//                         g[row] = first ? row_r : g[row] + row_r; then g[row] /= W on the first
+//                         entries (div > 0)
 //
 // Every rank runs the same launches on the same gathered bytes, so the gradient rows, the clip
 // norm over the union (lgcn_row_grad_norm with first_b) and the row Adam update are bitwise the

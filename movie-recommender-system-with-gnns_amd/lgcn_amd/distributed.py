@@ -10,8 +10,9 @@ clip_grad_norm_(1) + Adam step, so the replicated tables stay bitwise identical.
 With W = 1 this is exactly the reference step.
 
 With the row-lazy optimizer (lgcn_amd.optim.RowLazyAdam) the dense all_reduce is replaced by
-RowExchange: only the rows a step can make nonzero travel (all_gather of packed rows), every
-rank sums them in rank order, and every rank updates exactly the union of the ranks' rows.
+RowExchange: only the rows a step can make nonzero travel (one all_gather per step of packed
+row records: ids and rows), every rank sums them in rank order, and every rank updates exactly
+the union of the ranks' rows.
 """
 from __future__ import annotations
 
