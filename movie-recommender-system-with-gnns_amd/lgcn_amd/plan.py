@@ -67,6 +67,11 @@ def slice_bytes_for(num_nodes: int, d: int) -> int:
     x = int(num_nodes) * int(d) * 4
     if x < 16 * 2**20 or x > 512 * 2**20:
         return 0
+    if x < 32 * 2**20:
+        # 16-32 MB tables (C2 at d = 32, the 1 x 2 grid's column share): 12 MB slices, i.e. 2 user +
+        # 1 item slice, beat 8 MB's 3 + 1 (bench.py --dim 32: 0.710 -> 0.690 ms per K=3 step,
+        # profiles/r02zz_narrow/); below 16 MB (d = 16) the plain schedule stays ahead
+        return 12 * 2**20
     return int(min(max(x // 8, 8 * 2**20), 24 * 2**20))
 
 
