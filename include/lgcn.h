@@ -337,8 +337,10 @@ int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, co
  *     mode 0: catch the rows up to *step (duplicates handled by claim stamps, claim initialised
  *     to -1); mode 1: catch up, then apply step *step + 1 with the gradient times clip[1]
  *     (clip nullable), then ++*step (rows must be unique); mode 2: every row of [0, n_rows) up
- *     to *step. last[r] = the last step applied to row r.
- *   lgcn_row_grad_norm: out = (||g over the listed rows||, min(max_norm / (norm + 1e-6), 1)). */
+ *     to *step; mode 3: as mode 1 after lgcn_row_grad_norm advanced *step already (catch up to
+ *     *step - 1, apply *step, no advance launch). last[r] = the last step applied to row r.
+ *   lgcn_row_grad_norm: out = (||g over the listed rows||, min(max_norm / (norm + 1e-6), 1));
+ *     step_advance (nullable): ++*step_advance in the same launch (then lgcn_row_adam mode 3). */
 int lgcn_adam_consts(float* consts, int64_t t0, int64_t t1, float lr, double beta1, double beta2,
                      lgcn_stream_t stream);
 int lgcn_row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_lo, float* m_hi, float* v_lo,
@@ -350,7 +352,8 @@ int lgcn_row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_l
 int lgcn_row_grad_norm_workspace_floats(void);
 int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
                        int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
-                       const uint8_t* skip_b, float max_norm, float* ws, float* out, lgcn_stream_t stream);
+                       const uint8_t* skip_b, float max_norm, float* ws, float* out, int64_t* step_advance,
+                       lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Recall@k (reference utils/train_test.py:165-212, compute_recall_at_k, called from evaluate

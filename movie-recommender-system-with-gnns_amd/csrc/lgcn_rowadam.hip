@@ -111,7 +111,9 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
     const int64_t i = int64_t(blockIdx.x) * GPB + g;
-    const int64_t t = step[0];
+    // mode 3: the update after lgcn_row_grad_norm already advanced the counter to t + 1
+    const bool upd = mode == 1 || mode == 3;
+    const int64_t t = step[0] - (mode == 3 ? 1 : 0);
     int64_t row;
     if (mode == 2) {
         if (i >= n_rows) return;
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
     }
     const int64_t from = int64_t(last[row]) + 1;
     const int64_t upto = t;  // zero-gradient replays through step t
-    const float coef = (mode == 1 && clip) ? clip[1] : 1.0f;
+    const float coef = (upd && clip) ? clip[1] : 1.0f;
     const int64_t d = T.d;
     float4* P = reinterpret_cast<float4*>(trow(T.p_lo, T.p_hi, T.split, row, d)) + l;
     float4* M = reinterpret_cast<float4*>(trow(T.m_lo, T.m_hi, T.split, row, d)) + l;
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
         }
     }
     int32_t now = static_cast<int32_t>(upto);
-    if (mode == 1) {
+    if (upd) {
         const float2 c = consts[t + 1];
         const float4* G = reinterpret_cast<const float4*>(trow(T.g_lo, T.g_hi, T.split, row, d)) + l;
 #pragma unroll
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
         }
         now = static_cast<int32_t>(t + 1);
     }
-    if (from <= upto || mode == 1) {
+    if (from <= upto || upd) {
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             P[q * LPR] = p[q];
@@ -207,7 +209,8 @@ __global__ __launch_bounds__(kBlock) void k_row_sqnorm(RowTables T, RowList L, f
 }
 
 __global__ __launch_bounds__(kBlock) void k_norm_finish_rows(const float* __restrict__ partial, int nparts,
-                                                             float max_norm, float* __restrict__ out) {
+                                                             float max_norm, float* __restrict__ out,
+                                                             int64_t* __restrict__ step_advance) {
     __shared__ float red[kBlock / 64];
     float acc = 0.f;
     for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += partial[i];
@@ -221,6 +224,7 @@ __global__ __launch_bounds__(kBlock) void k_norm_finish_rows(const float* __rest
         const float coef = max_norm / (norm + 1e-6f);
         out[0] = norm;
         out[1] = coef < 1.0f ? coef : 1.0f;
+        if (step_advance) step_advance[0] += 1;  // the step the update (mode 3) then applies
     }
 }
 
@@ -243,10 +247,11 @@ int launch_row_adam(const RowTables& T, const RowList& L, int64_t n_rows, int32_
 }
 
 template <int LPR, int NV>
-int launch_row_norm(const RowTables& T, const RowList& L, float max_norm, float* ws, float* out, hipStream_t s) {
+int launch_row_norm(const RowTables& T, const RowList& L, float max_norm, float* ws, float* out, int64_t* step,
+                    hipStream_t s) {
     k_row_sqnorm<LPR, NV><<<kRowNormBlocks, kBlock, 0, s>>>(T, L, ws);
     if (int rc = check_launch("k_row_sqnorm")) return rc;
-    k_norm_finish_rows<<<1, kBlock, 0, s>>>(ws, kRowNormBlocks, max_norm, out);
+    k_norm_finish_rows<<<1, kBlock, 0, s>>>(ws, kRowNormBlocks, max_norm, out, step);
     return check_launch("k_norm_finish_rows");
 }
 
@@ -292,8 +297,8 @@ int lgcn_row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_l
                   float beta2, float one_minus_beta2, float eps, const float* clip, int32_t mode,
                   lgcn_stream_t stream) {
     RowTables T{p_lo, p_hi, g_lo, g_hi, m_lo, m_hi, v_lo, v_hi, split, d};
-    if (int rc = check_tables(T, mode == 1)) return rc;
-    if (mode < 0 || mode > 2 || !last || !step || !consts || (mode == 0 && !claim) || n_a < 0 || n_b < 0 ||
+    if (int rc = check_tables(T, mode == 1 || mode == 3)) return rc;
+    if (mode < 0 || mode > 3 || !last || !step || !consts || (mode == 0 && !claim) || n_a < 0 || n_b < 0 ||
         (n_a > 0 && !rows_a) || (n_b > 0 && !keys_b))
         return fail(LGCN_E_ARG, "lgcn_row_adam: bad args");
     RowList L{rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b};
@@ -317,7 +322,8 @@ int lgcn_row_grad_norm_workspace_floats(void) { return kRowNormBlocks; }
 
 int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
                        int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
-                       const uint8_t* skip_b, float max_norm, float* ws, float* out, lgcn_stream_t stream) {
+                       const uint8_t* skip_b, float max_norm, float* ws, float* out, int64_t* step_advance,
+                       lgcn_stream_t stream) {
     RowTables T{nullptr, nullptr, const_cast<float*>(g_lo), const_cast<float*>(g_hi), nullptr, nullptr, nullptr,
                 nullptr, split, d};
     if (!g_lo || !ws || !out || n_a < 0 || n_b < 0 || (n_a > 0 && !rows_a) || (n_b > 0 && !keys_b))
@@ -325,7 +331,7 @@ int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int3
     if (!al16(g_lo) || (g_hi && !al16(g_hi))) return fail(LGCN_E_UNSUPPORTED, "lgcn_row_grad_norm: alignment");
     RowList L{rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b};
     hipStream_t s = as_stream(stream);
-#define LGCN_RN(LP, NVV) launch_row_norm<LP, NVV>(T, L, max_norm, ws, out, s)
+#define LGCN_RN(LP, NVV) launch_row_norm<LP, NVV>(T, L, max_norm, ws, out, step_advance, s)
     LGCN_ROW_DISPATCH(LGCN_RN)
 #undef LGCN_RN
 }

@@ -77,7 +77,7 @@ _SIGS = {
     "lgcn_row_adam": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64,
                        _vp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _i32, _vp], ctypes.c_int),
     "lgcn_row_grad_norm_workspace_floats": ([], ctypes.c_int),
-    "lgcn_row_grad_norm": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp],
+    "lgcn_row_grad_norm": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp],
                            ctypes.c_int),
     "lgcn_rows_pack": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
                        ctypes.c_int),

@@ -150,7 +150,7 @@ class RowLazyAdam:
         b1, b2 = self.betas
         na = rows_a.numel() if rows_a is not None else 0
         nb = keys_b.numel() if keys_b is not None else 0
-        _ffi.check(lib.lgcn_row_adam(*self._tables(mode == 1), _ffi.ptr(rows_a), na, _ffi.ptr(keys_b), nb, off_b,
+        _ffi.check(lib.lgcn_row_adam(*self._tables(mode in (1, 3)), _ffi.ptr(rows_a), na, _ffi.ptr(keys_b), nb, off_b,
                                      _ffi.ptr(first_b), _ffi.ptr(skip_b), n_rows, self.last.data_ptr(),
                                      self.claim.data_ptr(), self.step_dev.data_ptr(), self.consts.data_ptr(),
                                      1 - b1, b2, 1 - b2, self.eps, _ffi.ptr(clip), mode,
@@ -175,10 +175,13 @@ class RowLazyAdam:
             _ffi.check(lib.lgcn_row_grad_norm(self.gu.data_ptr(), self.gi.data_ptr(), self.U, self.d,
                                               _ffi.ptr(rows_a), na, _ffi.ptr(keys_b), nb, off_b, _ffi.ptr(first_b),
                                               _ffi.ptr(skip_b), float(self.max_grad_norm), self.norm_ws.data_ptr(),
-                                              self.last_norm.data_ptr(), _ffi.stream_of(self.device)),
+                                              self.last_norm.data_ptr(), self.step_dev.data_ptr(),
+                                              _ffi.stream_of(self.device)),
                        "lgcn_row_grad_norm")
             clip = self.last_norm
-        self._row_adam(rows_a, keys_b, off_b, first_b, skip_b, 0, clip, 1)
+        # with the clip norm, its finishing launch also advances the device step counter (mode 3:
+        # one launch fewer per step); without it the update advances it itself (mode 1)
+        self._row_adam(rows_a, keys_b, off_b, first_b, skip_b, 0, clip, 1 if clip is None else 3)
         self.steps += 1
 
     def flush(self) -> None:
