@@ -3,7 +3,8 @@
 clip_grad_norm_(1), Adam step) as a fixed sequence of HIP launches.
 
     out  = LightGCN forward over the batch edges       (lgcn_spmm x K over a touched-only plan)
-    neg  = torch.randint(0, I, (B,))                   (same draw as reference sample_negative)
+    neg  = torch.randint(0, I, (B,))                   (same draw as reference sample_negative;
+                                                        eager before a graph replay)
     loss, per-triplet grad rows = lgcn_bpr_fused       (+ lgcn_bpr_loss)
     g    = scaled dF rows in a fixed order, written    (lgcn_csr_build over the 3B keys +
            straight into the two gradient tables        lgcn_segment_rows with the backward scale)
@@ -190,7 +191,15 @@ class FusedTrainStep:
                 self._states.pop(k)
         return st
 
-    def compute_grads(self, batch) -> torch.Tensor:
+    def _draw(self, st) -> None:
+        """This step's negatives (reference utils/helpers.py:64-82: torch.randint(0, I, (B,))).
+        Graph replays draw them eagerly just before the replay: a captured draw makes every
+        replay launch the generator's seed/offset fills first (two small kernels, ~9 us per C3
+        step, profiles/r02zz_graph_rng/), and the values are the same draws either way."""
+        m = self.model
+        torch.randint(0, m.num_items, (st.B,), device=m.user_embedding.weight.device, out=st.neg)
+
+    def compute_grads(self, batch, draw: bool = True) -> torch.Tensor:
         m = self.model
         ei = batch.edge_index
         st = self.state(ei)
@@ -204,8 +213,9 @@ class FusedTrainStep:
         div = float(K + 1)
         mul = float(np.float32(1.0 / (K + 1)))
         with torch.no_grad():
+            if draw:
+                self._draw(st)
             out = propagate_forward(uw.detach(), iw.detach(), st.plan, K)
-            torch.randint(0, I, (B,), device=dev, out=st.neg)
             if not st.small:  # only the all-keys sort reads the negatives' global row keys
                 torch.add(st.neg, U, out=st.keys[2 * B:])
             _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
@@ -248,17 +258,17 @@ class FusedTrainStep:
         iw.grad = gi
         return st.loss
 
-    def _step_lazy(self, st: _BatchState) -> torch.Tensor:
+    def _step_lazy(self, st: _BatchState, draw: bool = True) -> torch.Tensor:
         """The whole batch step with the row-lazy optimizer: catch the batch's rows (touched rows
         and this step's negatives) up, forward, loss, gradient rows written only where the step
         can make them nonzero, backward, [row exchange], clip + Adam on exactly those rows."""
-        loss = self._lazy_grads(st)
+        loss = self._lazy_grads(st, draw)
         if self.exchange is not None:
             self.exchange.gather()
         self._lazy_update(st)
         return loss
 
-    def _lazy_grads(self, st: _BatchState) -> torch.Tensor:
+    def _lazy_grads(self, st: _BatchState, draw: bool = True) -> torch.Tensor:
         m = self.model
         opt = self.optimizer
         lib = _ffi.load()
@@ -272,7 +282,8 @@ class FusedTrainStep:
         mul = float(np.float32(1.0 / (K + 1)))
         big = 1 << 62
         with torch.no_grad():
-            torch.randint(0, I, (B,), device=dev, out=st.neg)
+            if draw:
+                self._draw(st)
             opt.catch_up(st.touched_rows, st.neg, U)
             out = propagate_forward(uw.detach(), iw.detach(), st.plan, K)
             _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
@@ -364,10 +375,10 @@ class FusedTrainStep:
                 g = torch.cuda.CUDAGraph()
                 if self.exchange is None:
                     with torch.cuda.graph(g):
-                        st.graph_loss = self._step_lazy(st)
+                        st.graph_loss = self._step_lazy(st, draw=False)
                 else:  # two halves: the all_gather between them runs eagerly
                     with torch.cuda.graph(g):
-                        st.graph_loss = self._lazy_grads(st)
+                        st.graph_loss = self._lazy_grads(st, draw=False)
                     st.graph_post = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(st.graph_post):
                         self._lazy_update(st)
@@ -376,6 +387,7 @@ class FusedTrainStep:
                 return loss
             if self.optimizer.steps + 1 > self.optimizer.max_steps:
                 raise RuntimeError("RowLazyAdam: max_steps exceeded")
+            self._draw(st)
             st.graph.replay()
             if self.exchange is not None:
                 self.exchange.gather()
@@ -398,12 +410,13 @@ class FusedTrainStep:
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                st.graph_loss = self.compute_grads(batch)
+                st.graph_loss = self.compute_grads(batch, draw=False)
                 st.graph_grads = (self.model.user_embedding.weight.grad, self.model.item_embedding.weight.grad)
                 if self.world == 1:
                     self._optimize()
             st.graph = g
             return loss
+        self._draw(st)
         st.graph.replay()
         m = self.model
         m.user_embedding.weight.grad, m.item_embedding.weight.grad = st.graph_grads
