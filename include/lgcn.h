@@ -38,7 +38,7 @@ extern "C" {
 
 typedef void* lgcn_stream_t; /* a hipStream_t; NULL = the null stream */
 
-#define LGCN_ABI_VERSION 2
+#define LGCN_ABI_VERSION 3
 
 #define LGCN_OK 0
 #define LGCN_E_ARG (-1)         /* bad size / null pointer / unsupported argument */

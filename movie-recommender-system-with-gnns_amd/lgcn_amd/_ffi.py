@@ -23,7 +23,7 @@ EPI_SCALE = 5
 
 ITEM_BYTES = 16   # lgcn_item_t {int64 beg; int32 len; int32 dst}
 SPLIT_BYTES = 16  # lgcn_split_t {int32 row, pbeg, pcnt, pad}
-ABI_VERSION = 2  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
+ABI_VERSION = 3  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
 
 _lib = None
 
