@@ -6,13 +6,16 @@ fp32. One step = one full K-layer forward propagation (LightGCN.forward semantic
 models/light_gcn.py:28-40) with the plan (CSR + gcn_norm + schedule) already built and the
 embedding tables resident in HBM. value = K * E / wall time per step: ONE graph at every N.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
-GPU, strong scaling. C2 is sharded over an R x F grid (lgcn_amd.sharded): F column groups (each
-propagates d/F columns, no exchange between them) times R row groups (each rank propagates its
-own edge-balanced destination rows of the same graph, and each layer's two output blocks (user
-rows, item rows) are all-gathered over RCCL within the column group on a side stream while the
-other half-layer computes); the result is bitwise the 1-GPU result. C5 (--config c5) is feature-sharded: d/N columns per
-rank, no collective. The barrier and the max-over-ranks time go over RCCL.
+Multi-GPU: `python bench.py --gpus N` starts N rank processes itself (one per GPU; under
+torchrun, which sets WORLD_SIZE, it is one of them). Strong scaling. C2 is sharded over an R x F
+grid (lgcn_amd.sharded): F column groups (each propagates d/F columns, no exchange between them)
+times R row groups (each rank propagates its own edge-balanced destination rows of the same
+graph, and each layer's two output blocks (user rows, item rows) are all-gathered over RCCL within
+the column group on a side stream while the other half-layer computes). With R = 1 a rank's
+columns are bitwise the 1-GPU result; with R > 1 ranks run the plain schedule at chunk 128, whose
+rows are within 1e-5 of the sliced 1-GPU result (bitwise the 1-GPU plain schedule at that chunk).
+C5 (--config c5) is feature-sharded: d/N columns per rank, no collective. The barrier and the
+max-over-ranks time go over RCCL.
 
 Also reported (one JSON line on rank 0):
   roofline     — the dominant kernel (the item pass, k_spmm_vec; at C2 one launch per source
@@ -85,17 +88,42 @@ class LaunchTimer:
         return sum(s.elapsed_time(e) for s, e, _ in self.pairs) / sum(n for _, _, n in self.pairs)
 
 
-def load_traffic(workload: str):
-    """HBM bytes per launch of the dominant kernel from a committed PMC profile (or None)."""
+def kernel_source_sha16() -> str:
+    """sha256 prefix of the dominant kernel's source (csrc/lgcn_spmm.hip + the shared header)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ("lgcn_spmm.hip", "lgcn_common.h"):
+        h.update((ROOT / "movie-recommender-system-with-gnns_amd" / "csrc" / f).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def traffic_signature(workload: str, kernel: str, launches: int, n_items: int, edges: int, graph: dict) -> dict:
+    """What a PMC traffic entry was measured on: the workload, the kernel instance, the launch
+    schedule (launches per layer, items and edges of one layer's item pass), the graph's degree
+    statistics and the kernel source. A committed entry counts only when every field matches."""
+    return {"workload": workload, "kernel": kernel, "launches_per_layer": int(launches),
+            "items_per_layer": int(n_items), "edges_per_layer": int(edges), "graph": graph,
+            "kernel_source_sha16": kernel_source_sha16()}
+
+
+def load_traffic(signature: dict):
+    """(memory-side bytes per launch of the dominant kernel from the committed PMC profile, or None;
+    why not) — None unless the entry's recorded signature equals this run's."""
     p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
-        return None
+        return None, "no profiles/pmc_traffic.json"
     try:
-        data = json.loads(p.read_text())
-        ent = data.get(workload)
-        return None if ent is None else ent.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+        ent = json.loads(p.read_text()).get(signature["workload"])
+    except (OSError, ValueError) as e:
+        return None, f"unreadable pmc_traffic.json: {e}"
+    if ent is None:
+        return None, "no PMC entry for this workload"
+    rec = ent.get("signature")
+    if rec != signature:
+        diff = sorted(k for k in set(signature) | set(rec or {}) if (rec or {}).get(k) != signature.get(k))
+        return None, f"PMC entry measured on another plan/kernel (differs in: {', '.join(diff)})"
+    return ent.get("hbm_bytes_per_launch"), None
 
 
 def kernel_lpr(d):
@@ -105,12 +133,100 @@ def kernel_lpr(d):
 
 
 def init_dist(backend, dev):
+    import datetime
+
     import torch.distributed as dist
 
+    # a bounded timeout: a rank stuck in a collective ends the run instead of holding the node
+    timeout = datetime.timedelta(seconds=int(os.environ.get("LGCN_DIST_TIMEOUT_S", "300")))
     if backend == "nccl":
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("nccl", device_id=dev, timeout=timeout)
     else:
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, timeout=timeout)
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def child_envs(n: int, port: int, base=None) -> list:
+    """The environment of each of n rank processes (what torch.distributed.run would set):
+    RANK = LOCAL_RANK = i, WORLD_SIZE = LOCAL_WORLD_SIZE = n, rendezvous on 127.0.0.1:port."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for i in range(n):
+        e = dict(base)
+        e.update(RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(n: int, argv: list, script=None) -> int:
+    """`python bench.py --gpus N` outside torchrun: start N rank processes of this script (one per
+    GPU, LOCAL_RANK = GPU index) and wait for them. This process touches no GPU (it imports neither
+    torch nor lgcn_amd). Rank 0's stdout (the JSON line) is relayed; if any rank fails the others
+    are stopped and its exit code is returned. script: the rank program (tests; default this file)."""
+    import signal
+    import subprocess
+
+    port = free_port()
+    cmd = [sys.executable, "-u", str(script or pathlib.Path(__file__).resolve()), *argv]
+    log(f"launch: {n} rank processes on 127.0.0.1:{port}: {' '.join(cmd[2:])}")
+    procs = [subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if i == 0 else subprocess.DEVNULL,
+                              start_new_session=True)
+             for i, e in enumerate(child_envs(n, port))]
+    import threading
+
+    out = []
+
+    def relay():
+        # the JSON line to stdout; anything else a library prints there (gloo, RCCL) to stderr
+        for line in procs[0].stdout:
+            if line.lstrip().startswith(b"{"):
+                out.append(line)
+                sys.stdout.buffer.write(line)
+                sys.stdout.flush()
+            else:
+                sys.stderr.buffer.write(line)
+                sys.stderr.flush()
+
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    rc, stop_at = 0, None
+    pending = set(range(n))
+    while pending:
+        for i in sorted(pending):
+            r = procs[i].poll()
+            if r is None:
+                continue
+            pending.discard(i)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                stop_at = time.monotonic()
+                log(f"launch: rank {i} exited with {r}; stopping the other ranks")
+                for j in pending:
+                    try:
+                        os.killpg(procs[j].pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        if stop_at is not None and pending and time.monotonic() - stop_at > 30:
+            for j in pending:  # ranks that ignore SIGTERM (stuck in a collective)
+                try:
+                    os.killpg(procs[j].pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+            stop_at = time.monotonic()
+        time.sleep(0.2)
+    t.join(timeout=10)
+    if rc == 0 and not out:
+        log("launch: rank 0 printed nothing")
+        rc = 1
+    return rc
 
 
 def cpu_share():
@@ -208,7 +324,7 @@ def schedule_traffic(sched, n_src_rows: int, d: int):
         edges = int(ld[:, 0].sum())
     per_layer = (n_src_rows * row + edges * 8 + n * 16 + finished * 3 * row + run_rw * row
                  + sched.n_partials * row)
-    return per_layer, launches, edges, finished + sched.n_splits
+    return per_layer, launches, edges, finished + sched.n_splits, n
 
 
 def main():
@@ -246,6 +362,9 @@ def main():
                     help="train: reference-style step (compute_embeddings + bpr_loss + autograd) instead of "
                          "the fused no-autograd step")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # plain `python bench.py --gpus N`: become the launcher of N ranks (torchrun sets WORLD_SIZE)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     if args.workload == "train":
         return run_train(args)
 
@@ -334,7 +453,7 @@ def main():
                         mode=mode, step=lambda: propagate_forward_sharded(x0p, splan, K, ex))
 
         def trial_ms(st, n=8):
-            """max-over-ranks ms per step of a candidate grid (untimed by the bench line)."""
+            """This rank's ms per step of a candidate grid (untimed by the bench line)."""
             with torch.no_grad():
                 for _ in range(2):
                     st["step"]()
@@ -344,27 +463,44 @@ def main():
                 for _ in range(n):
                     st["step"]()
                 torch.cuda.synchronize()
-                t = torch.tensor([(time.perf_counter() - t) / n * 1e3], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            return float(t.item())
+            return (time.perf_counter() - t) / n * 1e3
 
         if args.shard:
             R, F = (int(v) for v in args.shard.split("x"))
             st = build_grid(R, F, args.exchange_mode)
         else:
             # the grid is picked by measurement: the compute per rank is known on one GPU
-            # (tools/shard_rank_probe.py), the exchange cost only on the node's xGMI links
+            # (tools/shard_rank_probe.py), the exchange cost only on the node's xGMI links.
+            # A candidate that raises on any rank is skipped on every rank (the ranks agree through
+            # one all_reduce of [ms, failed] per candidate), so one bad grid cannot end the run.
             st, best, grid_trials = None, None, {}
             for R, F, mode in grid_candidates(world, d_full):
-                cand = build_grid(R, F, mode)
-                ms = trial_ms(cand)
-                grid_trials[f"{R}x{F}" + (f"/{mode}" if mode else "")] = round(ms, 4)
-                log(f"[rank {rank}] grid trial {R}x{F} {mode or ''}: {ms:.3f} ms per step")
+                name = f"{R}x{F}" + (f"/{mode}" if mode else "")
+                cand, ms, failed = None, 0.0, 0.0
+                try:
+                    cand = build_grid(R, F, mode)
+                    ms = trial_ms(cand)
+                except Exception as e:  # noqa: BLE001 — logged, agreed on, skipped
+                    failed = 1.0
+                    log(f"[rank {rank}] grid trial {name} failed: {type(e).__name__}: {e}")
+                    torch.cuda.synchronize()
+                agree = torch.tensor([ms, failed], dtype=torch.float64, device=dev)
+                dist.all_reduce(agree, op=dist.ReduceOp.MAX)
+                ms, failed = float(agree[0].item()), bool(agree[1].item())
+                if failed:
+                    grid_trials[name] = "failed"
+                    cand = None
+                    torch.cuda.empty_cache()
+                    continue
+                grid_trials[name] = round(ms, 4)
+                log(f"[rank {rank}] grid trial {name}: {ms:.3f} ms per step")
                 if best is None or ms < best:
                     st, best = cand, ms
                 else:
                     del cand
                 torch.cuda.empty_cache()
+            if st is None:
+                raise SystemExit("every grid candidate failed")
         del user_w, item_w
         grid, shards, splan, exchange, step = st["grid"], st["shards"], st["splan"], st["ex"], st["step"]
         c0, c1 = grid.cols
@@ -429,10 +565,11 @@ def main():
     # one graph in every configuration: C2 on an R x F grid / C5 column-sharded over the ranks
     value = K * E * args.steps / elapsed
     # bytes of one middle layer's item pass (this rank's rows), spread over its launches
-    comp_layer, launches, e_mine, n_mine = 0, 0, 0, 0
+    comp_layer, launches, e_mine, n_mine, items_mine = 0, 0, 0, 0, 0
     for sc in scheds:
-        b, n, e_s, r_s = schedule_traffic(sc, N, d)
+        b, n, e_s, r_s, it = schedule_traffic(sc, N, d)
         comp_layer, launches, e_mine, n_mine = comp_layer + b, launches + n, e_mine + e_s, n_mine + r_s
+        items_mine += it
     comp_launch = comp_layer / launches
     # SURVEY §8d's no-reuse algorithmic bytes (every gathered row counted per edge) of this rank's rows
     alg_launch = (e_mine * (4 * d + 8) + n_mine * (4 * d + 8)) / launches
@@ -442,14 +579,14 @@ def main():
         workload = f"C2_ml25m_shaped_K{K}_d{d_full}" + ("" if args.scale == 1.0 else f"_scale{args.scale}")
         if sharded:
             workload += f"_grid{grid.R}x{grid.F}"
-    if c5 and world > 1:
-        workload_pmc = None
-    else:
-        workload_pmc = workload
-    traffic = load_traffic(workload_pmc) if workload_pmc else None
+    sliced = isinstance(scheds[0], SlicedDirection)
+    kernel_name = (f"k_spmm_vec<{kernel_lpr(d)},sliced> (lgcn_spmm_run_slices, {launches} source-slice "
+                   f"launches per layer)" if sliced else f"k_spmm_vec<{kernel_lpr(d)}> (lgcn_spmm_items)")
+    graph_stats = (graph.degree_stats() if graph is not None else {"num_nodes": N, "num_edges": E})
+    signature = traffic_signature(workload, kernel_name, launches, items_mine, e_mine, graph_stats)
+    traffic, stale = load_traffic(signature)
     basis = "pmc_memory_side" if traffic else "compulsory"
     achieved = (traffic if traffic else comp_launch) / (kernel_ms * 1e-3) / 1e9
-    sliced = isinstance(scheds[0], SlicedDirection)
     result = {
         "metric": f"edges propagated/sec (K={K}, d={d_full})",
         "value": value,
@@ -466,7 +603,10 @@ def main():
                  if c5 else "synthetic (seeded ML-25M-shaped bipartite graph, one graph for all ranks; random "
                             "N(0,0.01) embeddings)"),
         "config": {"workload": workload, "num_users": U, "num_items": I, "num_edges": E, "layers": K, "dim": d_full,
-                   "chunk": chunk, "graphs": 1,
+                   "chunk": chunk, "graphs": 1, "degree_stats": graph_stats,
+                   "graph_generator": (f"synth.bipartite_device seed 0" if c5 else
+                                       f"synth.ml25m_shaped seed 0 (user Zipf alpha {synth.ML25M_USER_ALPHA}, "
+                                       f"offset {synth.ML25M_USER_OFFSET})"),
                    "parallelism": (f"feature-sharded over {world} GPU(s): {d} columns each, full plan per rank, "
                                    "no collective") if c5 else
                                   (f"{grid.R} row groups x {grid.F} column groups over {world} GPUs: each rank "
@@ -475,12 +615,15 @@ def main():
                                    (f"ranks of a column group exchange each exchanged layer's two row blocks "
                                     f"({args.dist_backend} {'all_gather' if st['mode'] == 'allgather' else 'sends to every peer'}"
                                     f"), each overlapped with the other half-layer; " if grid.R > 1 else "") +
-                                   "column groups exchange nothing; bitwise the 1-GPU result of its schedule"
+                                   "column groups exchange nothing; " +
+                                   ("bitwise the 1-GPU result" if grid.R == 1 else
+                                    "within 1e-5 per row of the sliced 1-GPU result (bitwise the 1-GPU plain "
+                                    "schedule at chunk 128)")
                                    if sharded else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "basis": basis,
-                     "kernel": (f"k_spmm_vec<{kernel_lpr(d)},sliced> (lgcn_spmm_run_slices, {launches} source-slice "
-                                f"launches per layer)" if sliced else f"k_spmm_vec<{kernel_lpr(d)}> (lgcn_spmm_items)"),
+                     "traffic_unused_because": stale, "signature": signature,
+                     "kernel": kernel_name,
                      "kernel_ms": kernel_ms, "kernel_ms_sampled": f"HIP events around each layer's launches, every {TIMER_EVERY}th timed step",
                      "launches_per_layer": launches,
                      "compulsory_bytes_per_launch": comp_launch,

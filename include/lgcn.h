@@ -86,6 +86,9 @@ enum {
 
 const char* lgcn_last_error(void);
 int lgcn_abi_version(void);
+/* sha256 (hex) of the sources this library was compiled from: every csrc translation unit,
+ * lgcn_common.h and this header (build provenance; lgcn_amd._ffi refuses a mismatch). */
+const char* lgcn_source_sha256(void);
 
 /* ---------------------------------------------------------------------------------------
  * CSR construction. Stable counting sort of the edge list by `key`:

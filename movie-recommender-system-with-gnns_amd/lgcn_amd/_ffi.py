@@ -37,6 +37,7 @@ _sz = ctypes.c_size_t
 _SIGS = {
     "lgcn_last_error": ([], ctypes.c_char_p),
     "lgcn_abi_version": ([], ctypes.c_int),
+    "lgcn_source_sha256": ([], ctypes.c_char_p),
     "lgcn_csr_workspace_size": ([_i64, _i64, ctypes.POINTER(_sz)], ctypes.c_int),
     "lgcn_csr_build": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
     "lgcn_inv_sqrt_degree": ([_vp, _i64, _vp, _vp], ctypes.c_int),
@@ -131,8 +132,41 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     if lib.lgcn_abi_version() != ABI_VERSION:
         raise LgcnError(f"liblgcn ABI version {lib.lgcn_abi_version()} != {ABI_VERSION}")
     if path is None:
+        built, here = lib.lgcn_source_sha256().decode(), source_sha256()
+        if built != here:
+            raise LgcnError(f"{p} was built from other sources (sha256 {built[:16]}…) than the tree it is loaded "
+                            f"from ({here[:16]}…): rebuild it with __graft_entry__.build()")
         _lib = lib
     return lib
+
+
+CSRC = _HERE.parent / "csrc"
+INCLUDE = _HERE.parent.parent / "include"
+# the translation units of liblgcn.so (lgcn_build.cpp carries the hash and is not hashed)
+SOURCES = ("lgcn_plan.hip", "lgcn_spmm.hip", "lgcn_optim.hip", "lgcn_bpr.hip", "lgcn_recall.hip", "lgcn_rowadam.hip",
+           "lgcn_exchange.hip", "lgcn_partition.cpp", "lgcn_sample.cpp")
+
+
+def source_sha256() -> str:
+    """sha256 of the library's sources: each csrc translation unit, lgcn_common.h, include/lgcn.h
+    (name and bytes of each, in that order)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in [CSRC / s for s in SOURCES] + [CSRC / "lgcn_common.h", INCLUDE / "lgcn.h"]:
+        h.update(f.name.encode() + b"\0")
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
+def built_sha256(path: os.PathLike | str | None = None) -> str | None:
+    """The source hash baked into a built library, read from the file (without loading it)."""
+    p = pathlib.Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        return None
+    data = p.read_bytes()
+    i = data.find(b"LGCN_SOURCE_SHA256=")
+    return data[i + 19:i + 19 + 64].decode() if i >= 0 else None
 
 
 def check(rc: int, what: str) -> None:

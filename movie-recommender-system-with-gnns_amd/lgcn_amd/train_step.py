@@ -365,7 +365,7 @@ class FusedTrainStep:
         if self.lazy:
             st = self.state(batch.edge_index)
             if not st.lazy:
-                raise ValueError("lazy step needs a batch with 2B <= N")
+                raise ValueError("lazy step needs a batch whose 3B contribution ids fit int32 (3B < 2^31)")
             if not self.graphs:
                 return self._step_lazy(st)
             if getattr(st, "graph", None) is None:

@@ -41,6 +41,24 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
 
+# sha256 of each reference file this script executes, pinned when the fixtures were made: the
+# reference tree is untrusted public content, so a file that changed is refused before it runs
+REF_SHA256 = {
+    "models/light_gcn.py": "a3177a4bc97a3bb9447a927717d0bf787b73bfc6f578df020a066e02fd1ff9a1",
+    "utils/train_test.py": "6d0a86e09aff1ddbc25d8f68780cf80eec754a46882cc4aaea63d115f750cd7d",
+    "utils/helpers.py": "986c99169ec54697227dd818421c8620e9cb16385b4aa0b98f006b06ed29dcba",
+}
+
+
+def check_reference_files() -> None:
+    import hashlib
+
+    for rel, want in REF_SHA256.items():
+        got = hashlib.sha256((REF / rel).read_bytes()).hexdigest()
+        if got != want:
+            raise SystemExit(f"/root/reference/{rel} changed (sha256 {got}); refusing to execute it")
+
+
 class Batch:
     """What the reference's train()/evaluate() need from a batch: .edge_index and .to()."""
 
@@ -62,6 +80,7 @@ def reference_lightgcn():
 
     if not REF.exists():
         raise SystemExit("/root/reference is not mounted: fixtures can only be made in the build container")
+    check_reference_files()
     saved = {k: sys.modules.get(k) for k in ("torch_geometric", "torch_geometric.nn")}
     pyg = types.ModuleType("torch_geometric")
     pyg_nn = types.ModuleType("torch_geometric.nn")
@@ -138,6 +157,7 @@ def harness():
 
     if not REF.exists():
         raise SystemExit("/root/reference is not mounted: harness fixtures can only be made in the build container")
+    check_reference_files()
     sys.path.insert(0, str(REF / "utils"))
     import helpers as ref_helpers  # reference utils/helpers.py
     import train_test as ref_tt  # reference utils/train_test.py

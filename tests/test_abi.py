@@ -111,3 +111,16 @@ def test_get_embeddings_semantics():
     assert m.get_embeddings(item_indices=torch.tensor([1]))[0] is None
     with pytest.warns(UserWarning):
         assert m.get_embeddings() == (None, None)
+
+
+def test_library_was_built_from_these_sources(monkeypatch):
+    """Build provenance: the library carries the sha256 of the sources it was compiled from, and
+    the loader refuses a library built from other sources (so GPU runs exercise a binary that
+    matches the tree next to it, whoever built it)."""
+    from lgcn_amd import _ffi
+
+    assert _ffi.built_sha256() == _ffi.source_sha256() == _ffi.load().lgcn_source_sha256().decode()
+    monkeypatch.setattr(_ffi, "_lib", None)
+    monkeypatch.setattr(_ffi, "source_sha256", lambda: "0" * 64)
+    with pytest.raises(_ffi.LgcnError, match="built from other sources"):
+        _ffi.load()

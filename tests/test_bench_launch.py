@@ -1,0 +1,77 @@
+"""bench.py as its own launcher: `python bench.py --gpus N` outside torchrun starts N rank
+processes (the driver's SCALE run calls it that way). CPU only: a stand-in rank program checks the
+environment each rank gets, the relay of rank 0's JSON line and the failure path; the rendezvous
+itself is exercised with a world-2 gloo barrier."""
+import importlib.util
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_under_test", ROOT / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+RANK_PROGRAM = r"""
+import json, os, sys
+import torch.distributed as dist
+keys = ["RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"]
+env = {k: os.environ.get(k) for k in keys}
+dist.init_process_group("gloo")
+dist.barrier()
+fail = os.environ.get("FAIL_RANK")
+if fail is not None and int(os.environ["RANK"]) == int(fail):
+    sys.exit(3)
+if int(os.environ["RANK"]) == 0:
+    print(json.dumps({"env": env, "world": dist.get_world_size(), "argv": sys.argv[1:]}), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_child_envs_match_torchrun():
+    b = _bench()
+    envs = b.child_envs(4, 29555, base={"PATH": "/usr/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    for e in envs:
+        assert e["WORLD_SIZE"] == "4" and e["LOCAL_WORLD_SIZE"] == "4"
+        assert e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29555"
+        assert e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e["PATH"] == "/usr/bin"
+
+
+def test_launch_relays_rank0_json(tmp_path, capfd):
+    b = _bench()
+    prog = tmp_path / "rank.py"
+    prog.write_text(RANK_PROGRAM)
+    os.environ.pop("FAIL_RANK", None)
+    rc = b.launch_ranks(2, ["--gpus", "2", "--steps", "3"], script=prog)
+    assert rc == 0
+    out = capfd.readouterr().out.strip().splitlines()
+    assert len(out) == 1
+    rec = json.loads(out[0])
+    assert rec["world"] == 2 and rec["env"]["RANK"] == "0" and rec["env"]["WORLD_SIZE"] == "2"
+    assert rec["argv"] == ["--gpus", "2", "--steps", "3"]
+
+
+def test_launch_fails_when_a_rank_fails(tmp_path, monkeypatch):
+    b = _bench()
+    prog = tmp_path / "rank.py"
+    prog.write_text(RANK_PROGRAM)
+    monkeypatch.setenv("FAIL_RANK", "1")
+    assert b.launch_ranks(2, [], script=prog) == 3
+
+
+def test_bench_main_becomes_the_launcher(tmp_path):
+    """`python bench.py --gpus 2` with no WORLD_SIZE re-runs itself as 2 ranks; a bad flag in the
+    ranks' argv makes every rank fail, and the launcher returns non-zero without touching a GPU."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--config", "c2", "--shard", "bad"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode != 0
+    assert "launch: 2 rank processes" in r.stderr

@@ -40,11 +40,26 @@ def main():
         for line in open(log):
             if line.startswith("expected_read_bytes"):
                 factor = float(line.split()[1]) / (statistics.median(cal_f) * 1024)
+    # the plan/kernel the counters were taken on: bench.py's roofline.signature of the profiled run
+    sig = None
+    for name in ("pmc_fetch.log", "pmc_write.log"):
+        lp = os.path.join(args.prof, name)
+        if os.path.exists(lp):
+            for line in open(lp):
+                if line.startswith("{"):
+                    rec = json.loads(line)
+                    s = rec.get("roofline", {}).get("signature")
+                    if sig is not None and s != sig:
+                        raise SystemExit(f"{name}: the two PMC passes ran different plans")
+                    sig = s
+    if sig is None or sig.get("workload") != args.workload:
+        raise SystemExit("no bench.py signature for this workload in the PMC pass logs")
     f = statistics.mean(fetch) * 1024 * factor
     w = statistics.mean(write) * 1024
     data[args.workload] = {
         "hbm_bytes_per_launch": f + w, "fetch_bytes_corrected": f, "write_bytes": w,
         "fetch_correction_factor": factor, "kernel": args.kernel, "launches_measured": len(fetch),
+        "signature": sig,
         "source": f"{os.path.relpath(args.prof, ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
         "note": "average memory-side (L2-miss) bytes per launch; FETCH_SIZE also counts Infinity-Cache hits, so "
                 "this bounds HBM traffic from above"}
