@@ -108,6 +108,19 @@ int lgcn_csr_build(const int64_t* key, const int64_t* other, int64_t E, int64_t 
                    int64_t* rowptr, int32_t* col, int32_t* eid, int64_t* err_count,
                    void* ws, size_t ws_bytes, lgcn_stream_t stream);
 
+/* Key grouping without a radix sort: rowptr[R+1] and perm[B] exactly as lgcn_csr_build(key, key,
+ * B, R, ...) writes rowptr and eid (positions b grouped by key[b], ascending b inside a key; an
+ * out-of-range key counts in *err_count and is grouped under key 0, as there). A counting sort:
+ * one atomic count per key, one scan, atomic placement, then each key's few positions put in
+ * ascending order. cursor: device int32[R] scratch. Meant for many keys over a small range with
+ * short groups (the per-step negatives, B ~ 1.8e5 over I = 59,047 items: ~3 per key); a group's
+ * ordering is quadratic in its length. B < 2^31, R < 2^31.
+ * Replaces: the per-step grouping that index_put_(accumulate) performs implicitly in the
+ * backward of compute_embeddings' negative-row gather (reference utils/train_test.py:128-132,
+ * negatives from utils/helpers.py:64-82). */
+int lgcn_group_keys(const int64_t* key, int64_t B, int64_t R, int64_t* rowptr, int32_t* perm, int32_t* cursor,
+                    int64_t* err_count, lgcn_stream_t stream);
+
 /* gcn_norm(add_self_loops=False), PyG 2.4.0: deg = in-degree (count of edges whose target
  * is the node), dis = deg^-1/2 with inf -> 0 (computed as 1/sqrt(deg), correctly rounded
  * twice, which is what torch's CPU pow(-0.5) yields), and edge weight

@@ -400,6 +400,94 @@ size_t sched_cub_bytes(int64_t E, int64_t N, int32_t chunk) {
     return m > c ? m : c;
 }
 
+
+// ---- key grouping (lgcn_group_keys): a counting sort in five stream-ordered steps ----
+// Every index a kernel writes through is checked against the range it must fall in; a check
+// that fails counts in err (and the write is dropped) instead of faulting.
+
+__device__ __forceinline__ int64_t group_key(const int64_t* __restrict__ key, int64_t b, int64_t R, bool& bad) {
+    const int64_t k = key[b];
+    bad = (k < 0) | (k >= R);
+    return bad ? 0 : k;  // lgcn_csr_build groups a bad key under 0
+}
+
+__global__ void k_group_count(const int64_t* __restrict__ key, int64_t B, int64_t R, int32_t* __restrict__ count,
+                              unsigned long long* __restrict__ err) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    unsigned long long bad_local = 0;
+    for (int64_t b = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; b < B; b += stride) {
+        bool bad;
+        const int64_t k = group_key(key, b, R, bad);
+        bad_local += bad;
+        atomicAdd(&count[k], 1);
+    }
+    if (bad_local) atomicAdd(err, bad_local);
+}
+
+// One workgroup: exclusive scan of count[0..R) in tiles of kScanBlock * 4; rowptr[r] and
+// cursor[r] = start of key r (cursor overwrites count in place), rowptr[R] = B.
+constexpr int kScanBlock = 1024;
+__global__ __launch_bounds__(kScanBlock) void k_group_scan(int32_t* __restrict__ count_cursor, int64_t R,
+                                                           int64_t* __restrict__ rowptr) {
+    using Scan = hipcub::BlockScan<int32_t, kScanBlock>;
+    __shared__ typename Scan::TempStorage tmp;
+    int32_t carry = 0;
+    for (int64_t base = 0; base < R; base += int64_t(kScanBlock) * 4) {
+        const int64_t i0 = base + int64_t(threadIdx.x) * 4;
+        int32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (i0 + j < R) ? count_cursor[i0 + j] : 0;
+        const int32_t mine = v[0] + v[1] + v[2] + v[3];
+        int32_t pre, total;
+        Scan(tmp).ExclusiveSum(mine, pre, total);
+        int32_t run = carry + pre;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (i0 + j < R) {
+                rowptr[i0 + j] = run;
+                count_cursor[i0 + j] = run;
+            }
+            run += v[j];
+        }
+        carry += total;
+        __syncthreads();  // tmp is reused by the next tile
+    }
+    if (threadIdx.x == 0) rowptr[R] = carry;
+}
+
+__global__ void k_group_place(const int64_t* __restrict__ key, int64_t B, int64_t R,
+                              const int64_t* __restrict__ rowptr, int32_t* __restrict__ cursor,
+                              int32_t* __restrict__ perm, unsigned long long* __restrict__ err) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t b = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; b < B; b += stride) {
+        bool bad;
+        const int64_t k = group_key(key, b, R, bad);
+        const int32_t pos = atomicAdd(&cursor[k], 1);
+        if (pos < rowptr[k] || pos >= rowptr[k + 1]) {  // cannot happen when count and key agree
+            atomicAdd(err, 1ull);
+            continue;
+        }
+        perm[pos] = static_cast<int32_t>(b);
+    }
+}
+
+// Each key's positions in ascending order (insertion sort; groups are a few entries long).
+__global__ void k_group_order(const int64_t* __restrict__ rowptr, int64_t R, int32_t* __restrict__ perm) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < R; r += stride) {
+        const int64_t beg = rowptr[r], end = rowptr[r + 1];
+        for (int64_t i = beg + 1; i < end; ++i) {
+            const int32_t v = perm[i];
+            int64_t j = i - 1;
+            while (j >= beg && perm[j] > v) {
+                perm[j + 1] = perm[j];
+                --j;
+            }
+            perm[j + 1] = v;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -455,6 +543,28 @@ int lgcn_csr_build(const int64_t* key, const int64_t* other, int64_t E, int64_t 
     if (int rc = check_launch("k_rowptr_from_sorted")) return rc;
     k_gather_col<<<grid_for(E, kBlock, 8192), kBlock, 0, s>>>(other, eid, E, N, col);
     return check_launch("k_gather_col");
+}
+
+int lgcn_group_keys(const int64_t* key, int64_t B, int64_t R, int64_t* rowptr, int32_t* perm, int32_t* cursor,
+                    int64_t* err_count, lgcn_stream_t stream) {
+    if (B < 0 || R < 1 || !rowptr || !err_count || !cursor || (B > 0 && (!key || !perm)))
+        return fail(LGCN_E_ARG, "lgcn_group_keys: bad args");
+    if (B > INT32_MAX || R > INT32_MAX)
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_group_keys: B=%lld R=%lld exceed int32", (long long)B, (long long)R);
+    hipStream_t s = as_stream(stream);
+    if (int rc = check_hip(hipMemsetAsync(cursor, 0, sizeof(int32_t) * R, s), "memset cursor")) return rc;
+    auto* err = reinterpret_cast<unsigned long long*>(err_count);
+    if (B > 0) {
+        k_group_count<<<grid_for(B, kBlock, 4096), kBlock, 0, s>>>(key, B, R, cursor, err);
+        if (int rc = check_launch("k_group_count")) return rc;
+    }
+    k_group_scan<<<1, kScanBlock, 0, s>>>(cursor, R, rowptr);
+    if (int rc = check_launch("k_group_scan")) return rc;
+    if (B == 0) return LGCN_OK;
+    k_group_place<<<grid_for(B, kBlock, 4096), kBlock, 0, s>>>(key, B, R, rowptr, cursor, perm, err);
+    if (int rc = check_launch("k_group_place")) return rc;
+    k_group_order<<<grid_for(R, kBlock, 4096), kBlock, 0, s>>>(rowptr, R, perm);
+    return check_launch("k_group_order");
 }
 
 int lgcn_inv_sqrt_degree(const int64_t* rowptr_fwd, int64_t N, float* dis, lgcn_stream_t stream) {

@@ -40,6 +40,7 @@ _SIGS = {
     "lgcn_source_sha256": ([], ctypes.c_char_p),
     "lgcn_csr_workspace_size": ([_i64, _i64, ctypes.POINTER(_sz)], ctypes.c_int),
     "lgcn_csr_build": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
+    "lgcn_group_keys": ([_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_inv_sqrt_degree": ([_vp, _i64, _vp, _vp], ctypes.c_int),
     "lgcn_edge_norm": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_schedule_workspace_size": ([_i64, _i64, _i32, ctypes.POINTER(_sz)], ctypes.c_int),

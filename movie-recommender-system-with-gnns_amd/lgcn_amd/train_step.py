@@ -69,16 +69,22 @@ class _BatchState:
         elif self.small:
             self.fixed_dense, self.fixed_sparse = segment_directions(self.keys[:2 * B], N, chunk=32)
         if self.small and B >= sorted_scatter_min_b():
-            # large B: the negatives are grouped by row with one stable radix sort per step
-            # (lgcn_csr_build over the B keys) and scattered row by row (lgcn_sorted_scatter_add)
+            # large B: the negatives are grouped by row once per step and scattered row by row
+            # (lgcn_sorted_scatter_add); the grouping is a counting sort (lgcn_group_keys) or,
+            # with LGCN_NEG_GROUPING=radix, one stable radix sort (lgcn_csr_build over the B keys)
+            # — the same rowptr / perm either way
             self.neg_rowptr = torch.empty(I + 1, dtype=torch.int64, device=dev)
-            self.neg_col = torch.empty(B, dtype=torch.int32, device=dev)
             self.neg_perm = torch.empty(B, dtype=torch.int32, device=dev)
             self.neg_err = torch.zeros(1, dtype=torch.int64, device=dev)
-            lib_ = _ffi.load()
-            nb = _ffi._sz(0)
-            _ffi.check(lib_.lgcn_csr_workspace_size(B, I, nb), "lgcn_csr_workspace_size")
-            self.neg_ws = torch.empty(max(1, nb.value), dtype=torch.uint8, device=dev)
+            self.neg_grouping = neg_grouping()
+            if self.neg_grouping == "radix":
+                self.neg_col = torch.empty(B, dtype=torch.int32, device=dev)
+                lib_ = _ffi.load()
+                nb = _ffi._sz(0)
+                _ffi.check(lib_.lgcn_csr_workspace_size(B, I, nb), "lgcn_csr_workspace_size")
+                self.neg_ws = torch.empty(max(1, nb.value), dtype=torch.uint8, device=dev)
+            else:
+                self.neg_cursor = torch.empty(max(1, I), dtype=torch.int32, device=dev)
         else:
             self.neg_rowptr = None
         if self.small:
@@ -106,6 +112,17 @@ class _BatchState:
         self.plan.bwd  # build the transposed plan now (its build reads counts back once)
 
 
+def neg_grouping() -> str:
+    """How the sorted negatives path groups the B keys by row: "count" (lgcn_group_keys, the
+    default) or "radix" (lgcn_csr_build); LGCN_NEG_GROUPING overrides."""
+    import os
+
+    g = os.environ.get("LGCN_NEG_GROUPING", "count")
+    if g not in ("count", "radix"):
+        raise ValueError(f"LGCN_NEG_GROUPING={g!r}: expected 'count' or 'radix'")
+    return g
+
+
 def sorted_scatter_min_b() -> int:
     """Batch size from which the negatives go through the sorted scatter instead of the range
     scatter (whose key streaming grows as B^2): measured on the C3 graphs (B ~ 1e4: range
@@ -129,9 +146,14 @@ def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: 
                                               st.overflow.data_ptr(), _ffi.ptr(store_unless), stream),
                    "lgcn_range_scatter_add")
         return
-    _ffi.check(lib.lgcn_csr_build(st.neg.data_ptr(), st.neg.data_ptr(), B, I, st.neg_rowptr.data_ptr(),
-                                  st.neg_col.data_ptr(), st.neg_perm.data_ptr(), st.neg_err.data_ptr(),
-                                  st.neg_ws.data_ptr(), st.neg_ws.numel(), stream), "lgcn_csr_build(negatives)")
+    if st.neg_grouping == "radix":
+        _ffi.check(lib.lgcn_csr_build(st.neg.data_ptr(), st.neg.data_ptr(), B, I, st.neg_rowptr.data_ptr(),
+                                      st.neg_col.data_ptr(), st.neg_perm.data_ptr(), st.neg_err.data_ptr(),
+                                      st.neg_ws.data_ptr(), st.neg_ws.numel(), stream), "lgcn_csr_build(negatives)")
+    else:
+        _ffi.check(lib.lgcn_group_keys(st.neg.data_ptr(), B, I, st.neg_rowptr.data_ptr(), st.neg_perm.data_ptr(),
+                                       st.neg_cursor.data_ptr(), st.neg_err.data_ptr(), stream),
+                   "lgcn_group_keys(negatives)")
     _ffi.check(lib.lgcn_sorted_scatter_add(st.neg_rowptr.data_ptr(), st.neg_perm.data_ptr(), I, U, C.data_ptr(), d,
                                            gu.data_ptr(), gi.data_ptr(), U, mul, div, *reg,
                                            st.c2buf.data_ptr(), st.c2flag.data_ptr(), _ffi.ptr(store_unless), stream),

@@ -103,18 +103,36 @@ def test_c3_training_step_matches_oracle(gpu, c3, monkeypatch):
         stats[name] = assert_rows_close(g_h.cpu().numpy(), g_r, what=f"C3 {name}")
     torch.nn.utils.clip_grad_norm_(ref.parameters(), max_norm=1)
     ropt.step()
-    for name, p_h, p_r in (("user", b.user_embedding.weight, ref.user_embedding.weight),
-                           ("item", b.item_embedding.weight, ref.item_embedding.weight)):
+    # (1) the optimizer alone: torch's clip_grad_norm_(1) + Adam(1e-3) applied on the CPU to the
+    # HIP gradient tables == the row-lazy HIP step's tables, every row within 1e-5 of its scale
+    # (rows that do not move must stay bitwise)
+    cp = [torch.nn.Parameter(w0[f"{n}_embedding.weight"].clone()) for n in ("user", "item")]
+    cp[0].grad = a.user_embedding.weight.grad.cpu().clone()
+    cp[1].grad = a.item_embedding.weight.grad.cpu().clone()
+    copt = torch.optim.Adam(cp, lr=1e-3)
+    torch.nn.utils.clip_grad_norm_(cp, max_norm=1)
+    copt.step()
+    for name, p_h, p_c in (("user", b.user_embedding.weight, cp[0]), ("item", b.item_embedding.weight, cp[1])):
+        assert_rows_close(p_h.detach().cpu().numpy(), p_c.detach().numpy(), what=f"C3 {name} Adam step on HIP grads")
+    # (2) end to end against the oracle harness: Adam's first step moves each weight by about
+    # lr * sign(grad), so every element whose oracle gradient is clear of the gradient parity bar
+    # (|g| > 1e-4 * max|g| of its row, ten times the 1e-5 per-row bar: its sign is settled) must
+    # land within 1e-5 of its row's scale; elements with noise-level gradients are counted
+    noise = {}
+    for name, p_h, p_r, g_r in (("user", b.user_embedding.weight, ref.user_embedding.weight, gu_r),
+                                ("item", b.item_embedding.weight, ref.item_embedding.weight, gi_r)):
         ph, pr, p0 = p_h.detach().cpu().numpy(), p_r.detach().numpy(), w0[f"{name}_embedding.weight"].numpy()
         moved_h, moved_r = np.any(ph != p0, axis=1), np.any(pr != p0, axis=1)
         # the same rows move (touched rows and the step's negatives)
         assert np.array_equal(moved_h, moved_r), (name, int(moved_h.sum()), int(moved_r.sum()))
-        # Adam's first step moves each weight by ~lr * sign(grad): elements whose gradient is
-        # within rounding of 0 may take the other sign, so bound the fraction that differ
-        diff = np.abs(ph - pr)
-        assert np.mean(diff <= 1e-6) > 0.999 and diff.max() <= 2.1e-3, (name, float(np.mean(diff <= 1e-6)))
+        settled = np.abs(g_r) > 1e-4 * np.abs(g_r).max(axis=1, keepdims=True)
+        diff = np.where(settled, np.abs(ph - pr), 0.0)
+        scale = np.abs(pr).max(axis=1)
+        worst = float((diff.max(axis=1) / np.where(scale > 0, scale, 1.0)).max())
+        assert worst <= 1e-5, (name, worst)
+        noise[name] = (int((~settled & (g_r != 0)).sum()), int((g_r != 0).sum()))
     print(f"C3 batch E={ei_np.shape[1]} f_intra={c3['f_intra']:.4f} loss {loss_a:.7f} vs {lr_:.7f}; "
-          f"grad row-rel {stats}")
+          f"grad row-rel {stats}; noise-level gradient elements (unchecked / nonzero) {noise}")
 
 
 def _free_port():

@@ -39,7 +39,9 @@ def test_c2_single_layer_bitwise_on_unsplit_rows(gpu, c2):
     """One layer: every row summed as one sequential chain (not cut into chunks — with the
     source-sliced schedule, a chain that runs through several slice launches) is bitwise the
     reference CPU scatter_add_ result; split (hub) rows — up to 62k terms each — are within 1e-5
-    relative and at least as close to the exact float64 sum as the sequential CPU order."""
+    relative and, against the exact float64 sums, no worse than the sequential CPU order: their
+    root-mean-square error over every split-row entry is at most the sequential order's (the
+    largest single-entry errors are printed next to each other)."""
     from lgcn_amd.propagate import lgconv_forward
 
     g, plan = c2
@@ -63,9 +65,11 @@ def test_c2_single_layer_bitwise_on_unsplit_rows(gpu, c2):
     rows = pos[dst[sel]]
     wx = w[sel].astype(np.float64)
     exact = np.stack([np.bincount(rows, weights=wx * x[src[sel], c], minlength=(~mask).sum()) for c in range(64)], 1)
-    err_hip = np.abs(y[~mask] - exact).max()
-    err_ref = np.abs(ref[~mask] - exact).max()
-    assert err_hip <= 1.5 * err_ref + 1e-12, (err_hip, err_ref)
+    e_hip, e_ref = y[~mask] - exact, ref[~mask] - exact
+    rms_hip, rms_ref = float(np.sqrt(np.mean(e_hip ** 2))), float(np.sqrt(np.mean(e_ref ** 2)))
+    print(f"split rows vs exact: rms {rms_hip:.3g} (chunked) vs {rms_ref:.3g} (sequential); "
+          f"max {np.abs(e_hip).max():.3g} vs {np.abs(e_ref).max():.3g}")
+    assert rms_hip <= rms_ref, (rms_hip, rms_ref)
 
 
 def test_c2_adjoint_and_linear(gpu, c2):

