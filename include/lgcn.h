@@ -370,6 +370,16 @@ int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int3
                        int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
                        const uint8_t* skip_b, float max_norm, float* ws, float* out, int64_t* step_advance,
                        lgcn_stream_t stream);
+/* The clip norm split for the owner-sharded exchange (each rank owns some rows; the norm is over
+ * all ranks' rows): lgcn_row_grad_sqnorm writes the lgcn_row_grad_norm_workspace_floats() block
+ * partials of the listed rows' sum of squares (fixed block assignment: deterministic for a
+ * fixed list); lgcn_row_grad_norm_finish sums nparts partials (e.g. every rank's, all-gathered,
+ * in rank order) and writes out / advances step_advance as lgcn_row_grad_norm does. */
+int lgcn_row_grad_sqnorm(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
+                         int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
+                         const uint8_t* skip_b, float* partials, lgcn_stream_t stream);
+int lgcn_row_grad_norm_finish(const float* partials, int64_t nparts, float max_norm, float* out, int64_t* step_advance,
+                              lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Recall@k (reference utils/train_test.py:165-212, compute_recall_at_k, called from evaluate
@@ -453,6 +463,36 @@ int lgcn_rows_mark_first(const int64_t* ids, int64_t n, int32_t* claim, uint8_t*
 int lgcn_rows_accumulate(const int64_t* ids, const float* rows, int64_t world, int64_t cap, int64_t rank_stride,
                          const uint8_t* first, float* g_lo, float* g_hi, int64_t split, int32_t d, float div,
                          lgcn_stream_t stream);
+
+/* Owner-sharded exchange (lgcn_amd.owner.OwnerExchange; the all_gather above replaced by two
+ * all_to_alls): row r is owned by rank r % world, which alone holds its Adam state and applies its
+ * update; each rank sends its gradient rows to their owners and asks the owners for the rows its
+ * next step reads. A send buffer is world destination blocks of block_floats floats:
+ *   [gradient ids: 2*cap floats (int64, -1 = empty) | gradient rows: cap*d | pad |
+ *    request ids at float offset req_off: 2*rcap floats (int64, -1 = empty) | pad]
+ *   lgcn_owner_reset: every id slot := -1, counts[0 .. 2*world) := 0.
+ *   lgcn_owner_pack_rows: each listed gradient row (the lgcn_row_adam list, first_b / skip_b
+ *     filters) into destination row % world at the next free slot (counts[o]); a full
+ *     destination sets *overflow |= 1 (the row is dropped: the caller must check).
+ *   lgcn_owner_pack_requests: each listed row id (rows_a, then keys_b + off_b; duplicates allowed)
+ *     into destination row % world's request slots (counts[world + o]) and mine[o*rcap + slot];
+ *     full: *overflow |= 2.
+ *   lgcn_rows_gather: rows[i] = p[ids[i]] for ids[i] >= 0 (scatter != 0: p[ids[i]] = rows[i]).
+ *   lgcn_rows_mark: mask[ids[i]] = value for ids[i] >= 0 (and first[i], if first is given).
+ * Replaces the same reference step as lgcn_rows_pack (utils/train_test.py:92-96 under DP). */
+int lgcn_owner_reset(float* send, int64_t world, int64_t block_floats, int64_t cap, int64_t req_off, int64_t rcap,
+                     int32_t* counts, lgcn_stream_t stream);
+int lgcn_owner_pack_rows(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
+                         int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
+                         const uint8_t* skip_b, int64_t world, int64_t cap, int64_t block_floats, int32_t* counts,
+                         float* send, int32_t* overflow, lgcn_stream_t stream);
+int lgcn_owner_pack_requests(const int32_t* rows_a, int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b,
+                             int64_t world, int64_t rcap, int64_t block_floats, int64_t req_off, int32_t* counts,
+                             float* send, int64_t* mine, int32_t* overflow, lgcn_stream_t stream);
+int lgcn_rows_gather(const float* p_lo, const float* p_hi, int64_t split, int32_t d, const int64_t* ids, int64_t n,
+                     float* rows, int32_t scatter, lgcn_stream_t stream);
+int lgcn_rows_mark(const int64_t* ids, const uint8_t* first, int64_t n, uint8_t* mask, int32_t value,
+                   lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Host-side (no GPU): balanced k-way node partition for Cluster-GCN batching, the METIS

@@ -17,6 +17,8 @@
 //
 // Rows live in two tables (r < split: lo[r], else hi[r - split]) like everywhere else.
 
+#include <climits>
+
 #include "lgcn_common.h"
 
 using namespace lgcn;
@@ -251,6 +253,7 @@ int launch_row_norm(const RowTables& T, const RowList& L, float max_norm, float*
                     hipStream_t s) {
     k_row_sqnorm<LPR, NV><<<kRowNormBlocks, kBlock, 0, s>>>(T, L, ws);
     if (int rc = check_launch("k_row_sqnorm")) return rc;
+    if (!out) return LGCN_OK;  // partials only (lgcn_row_grad_sqnorm)
     k_norm_finish_rows<<<1, kBlock, 0, s>>>(ws, kRowNormBlocks, max_norm, out, step);
     return check_launch("k_norm_finish_rows");
 }
@@ -326,7 +329,7 @@ int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int3
                        lgcn_stream_t stream) {
     RowTables T{nullptr, nullptr, const_cast<float*>(g_lo), const_cast<float*>(g_hi), nullptr, nullptr, nullptr,
                 nullptr, split, d};
-    if (!g_lo || !ws || !out || n_a < 0 || n_b < 0 || (n_a > 0 && !rows_a) || (n_b > 0 && !keys_b))
+    if (!g_lo || !ws || n_a < 0 || n_b < 0 || (n_a > 0 && !rows_a) || (n_b > 0 && !keys_b))
         return fail(LGCN_E_ARG, "lgcn_row_grad_norm: bad args");
     if (!al16(g_lo) || (g_hi && !al16(g_hi))) return fail(LGCN_E_UNSUPPORTED, "lgcn_row_grad_norm: alignment");
     RowList L{rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b};
@@ -334,6 +337,23 @@ int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int3
 #define LGCN_RN(LP, NVV) launch_row_norm<LP, NVV>(T, L, max_norm, ws, out, step_advance, s)
     LGCN_ROW_DISPATCH(LGCN_RN)
 #undef LGCN_RN
+}
+
+int lgcn_row_grad_sqnorm(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
+                         int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
+                         const uint8_t* skip_b, float* partials, lgcn_stream_t stream) {
+    if (!partials) return fail(LGCN_E_ARG, "lgcn_row_grad_sqnorm: null partials");
+    return lgcn_row_grad_norm(g_lo, g_hi, split, d, rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b, 0.0f, partials,
+                              nullptr, nullptr, stream);
+}
+
+int lgcn_row_grad_norm_finish(const float* partials, int64_t nparts, float max_norm, float* out, int64_t* step_advance,
+                              lgcn_stream_t stream) {
+    if (!partials || !out || nparts < 1 || nparts > INT32_MAX)
+        return fail(LGCN_E_ARG, "lgcn_row_grad_norm_finish: bad args");
+    k_norm_finish_rows<<<1, kBlock, 0, as_stream(stream)>>>(partials, static_cast<int>(nparts), max_norm, out,
+                                                           step_advance);
+    return check_launch("k_norm_finish_rows");
 }
 
 }  // extern "C"

@@ -81,6 +81,15 @@ _SIGS = {
     "lgcn_row_grad_norm_workspace_floats": ([], ctypes.c_int),
     "lgcn_row_grad_norm": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp],
                            ctypes.c_int),
+    "lgcn_row_grad_sqnorm": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _vp, _vp], ctypes.c_int),
+    "lgcn_row_grad_norm_finish": ([_vp, _i64, _f32, _vp, _vp, _vp], ctypes.c_int),
+    "lgcn_owner_reset": ([_vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp], ctypes.c_int),
+    "lgcn_owner_pack_rows": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _vp, _vp,
+                              _vp, _vp], ctypes.c_int),
+    "lgcn_owner_pack_requests": ([_vp, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp],
+                                 ctypes.c_int),
+    "lgcn_rows_gather": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i32, _vp], ctypes.c_int),
+    "lgcn_rows_mark": ([_vp, _vp, _i64, _vp, _i32, _vp], ctypes.c_int),
     "lgcn_rows_pack": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
                        ctypes.c_int),
     "lgcn_rows_mark_first": ([_vp, _i64, _vp, _vp, _vp], ctypes.c_int),

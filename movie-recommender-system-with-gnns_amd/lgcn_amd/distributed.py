@@ -96,6 +96,7 @@ class RowExchange:
         self.ids_all = torch.full((self.world * self.cap,), -1, dtype=torch.int64, device=device)
         self.first = torch.zeros(self.world * self.cap, dtype=torch.uint8, device=device)
         self.claim = torch.full((self.N,), 2**31 - 1, dtype=torch.int32, device=device)
+        self.bytes = 0  # received from peers over the run
 
     def rows_ptr(self) -> int:
         """device pointer of rank 0's rows in the gathered records."""
@@ -108,6 +109,7 @@ class RowExchange:
 
     def gather(self) -> None:
         """The collective (eager, between the step's two captured halves): one per step."""
+        self.bytes += (self.world - 1) * self.blk * 4
         if self.world == 1:
             self.pack_all.copy_(self.pack)
         elif dist.get_backend() == "nccl":

@@ -156,9 +156,37 @@ class RowLazyAdam:
                                      1 - b1, b2, 1 - b2, self.eps, _ffi.ptr(clip), mode,
                                      _ffi.stream_of(self.device)), "lgcn_row_adam")
 
-    def catch_up(self, rows_a: torch.Tensor, keys_b: torch.Tensor | None = None, off_b: int = 0) -> None:
-        """Bring the listed rows (duplicates allowed) up to the completed step count."""
-        self._row_adam(rows_a, keys_b, off_b, None, None, 0, None, 0)
+    def catch_up(self, rows_a: torch.Tensor | None, keys_b: torch.Tensor | None = None, off_b: int = 0,
+                 first_b: torch.Tensor | None = None) -> None:
+        """Bring the listed rows (duplicates allowed; list b filtered by first_b) up to the completed
+        step count."""
+        self._row_adam(rows_a, keys_b, off_b, first_b, None, 0, None, 0)
+
+    # --- the owner-sharded exchange's pieces (lgcn_amd.owner): the clip norm over every rank's rows
+    def sqnorm_partials(self, keys_b: torch.Tensor, skip_b: torch.Tensor, partials: torch.Tensor) -> None:
+        """Block partials of the sum of squares of the gradient rows keys_b[j] with !skip_b[row]."""
+        lib = _ffi.load()
+        _ffi.check(lib.lgcn_row_grad_sqnorm(self.gu.data_ptr(), self.gi.data_ptr(), self.U, self.d, None, 0,
+                                            keys_b.data_ptr(), keys_b.numel(), 0, None, skip_b.data_ptr(),
+                                            partials.data_ptr(), _ffi.stream_of(self.device)),
+                   "lgcn_row_grad_sqnorm")
+
+    def step_rows_with_partials(self, keys_b: torch.Tensor, first_b: torch.Tensor,
+                                partials_all: torch.Tensor | None) -> None:
+        """One Adam step on the list's first-occurrence rows, clipped by the norm finished from
+        every rank's partials (partials_all, rank order; None without clipping)."""
+        if self.steps + 1 > self.max_steps:
+            raise RuntimeError(f"RowLazyAdam: more than max_steps={self.max_steps} steps")
+        clip = None
+        if self.max_grad_norm is not None:
+            lib = _ffi.load()
+            _ffi.check(lib.lgcn_row_grad_norm_finish(partials_all.data_ptr(), partials_all.numel(),
+                                                     float(self.max_grad_norm), self.last_norm.data_ptr(),
+                                                     self.step_dev.data_ptr(), _ffi.stream_of(self.device)),
+                       "lgcn_row_grad_norm_finish")
+            clip = self.last_norm
+        self._row_adam(None, keys_b, 0, first_b, None, 0, clip, 1 if clip is None else 3)
+        self.steps += 1
 
     def step_rows(self, rows_a: torch.Tensor | None, keys_b: torch.Tensor | None = None, off_b: int = 0,
                   first_b: torch.Tensor | None = None, skip_b: torch.Tensor | None = None) -> None:

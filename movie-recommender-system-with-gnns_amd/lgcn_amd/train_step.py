@@ -174,13 +174,17 @@ class FusedTrainStep:
     compute_grads(batch) -> loss: sets user/item_embedding.weight.grad only."""
 
     def __init__(self, model, optimizer, bpr_coeff: float = 5e-3, world: int = 1, max_entries: int = 4096,
-                 graphs: bool = False, lazy: bool = False, exchange=None):
+                 graphs: bool = False, lazy: bool = False, exchange=None, neg_seed: int | None = None):
         """graphs=True: the first step of each batch runs eagerly, then the whole step (gradients
         and, at world == 1, the optimizer — which must be a capturable FusedAdam) is captured in a
         per-batch hipGraph and replayed from then on; negatives still come from the global CUDA
         generator (graph-safe Philox offsets), so each replay draws new ones.
-        exchange (lazy, data parallel): a lgcn_amd.distributed.RowExchange; the step is then two
-        captured halves around the eager all_gather of the packed gradient rows."""
+        exchange (lazy, data parallel): a lgcn_amd.distributed.RowExchange (replicated optimizer;
+        the step is two captured halves around the eager all_gather of the packed gradient rows) or
+        a lgcn_amd.owner.OwnerExchange (owner-sharded optimizer: step(batch, next_batch) — the
+        rows of next_batch's step are fetched from their owners at the end of this one).
+        neg_seed: draw step k's negatives from a generator seeded (neg_seed, k) instead of the
+        global CUDA generator (the same draws whichever exchange runs, and whenever they are drawn)."""
         self.model = model
         self.optimizer = optimizer
         self.coeff = float(bpr_coeff)
@@ -199,6 +203,15 @@ class FusedTrainStep:
         elif graphs and world == 1 and not getattr(optimizer, "capturable", False):
             raise ValueError("graphs=True needs a capturable optimizer (lgcn_amd.optim.FusedAdam(capturable=True))")
         self._states: dict[int, tuple[weakref.ref, int, _BatchState]] = {}
+        from .owner import OwnerExchange
+
+        self.owner = isinstance(exchange, OwnerExchange)
+        if self.owner and not lazy:
+            raise ValueError("an OwnerExchange needs lazy=True (RowLazyAdam)")
+        self.neg_seed = neg_seed
+        self._gen = None
+        self._k = 0  # steps taken (the index of the next step)
+        self._owner_graphs = None
 
     def state(self, edge_index: torch.Tensor) -> _BatchState:
         hit = self._states.get(id(edge_index))
@@ -213,13 +226,22 @@ class FusedTrainStep:
                 self._states.pop(k)
         return st
 
-    def _draw(self, st) -> None:
-        """This step's negatives (reference utils/helpers.py:64-82: torch.randint(0, I, (B,))).
+    def _draw(self, st, k: int | None = None) -> None:
+        """Step k's negatives (reference utils/helpers.py:64-82: torch.randint(0, I, (B,))).
         Graph replays draw them eagerly just before the replay: a captured draw makes every
         replay launch the generator's seed/offset fills first (two small kernels, ~9 us per C3
         step, profiles/r02zz_graph_rng/), and the values are the same draws either way."""
         m = self.model
-        torch.randint(0, m.num_items, (st.B,), device=m.user_embedding.weight.device, out=st.neg)
+        dev = m.user_embedding.weight.device
+        k = self._k if k is None else k
+        gen = None
+        if self.neg_seed is not None:
+            if self._gen is None:
+                self._gen = torch.Generator(device=dev)
+            self._gen.manual_seed(int(self.neg_seed) * 1_000_003 + int(k))
+            gen = self._gen
+        torch.randint(0, m.num_items, (st.B,), device=dev, out=st.neg, generator=gen)
+        st.neg_step = k
 
     def compute_grads(self, batch, draw: bool = True) -> torch.Tensor:
         m = self.model
@@ -306,7 +328,8 @@ class FusedTrainStep:
         with torch.no_grad():
             if draw:
                 self._draw(st)
-            opt.catch_up(st.touched_rows, st.neg, U)
+            if not self.owner:  # owner-sharded: the rows were fetched current by the previous step
+                opt.catch_up(st.touched_rows, st.neg, U)
             out = propagate_forward(uw.detach(), iw.detach(), st.plan, K)
             _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
                                           st.users.data_ptr(), st.pos.data_ptr(), st.neg.data_ptr(), B, d,
@@ -329,7 +352,16 @@ class FusedTrainStep:
                                                  st.c2flag.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U,
                                                  stream), "lgcn_flagged_rows_add")
             ex = self.exchange
-            if ex is not None:
+            if self.owner:
+                # this rank's rows with a possibly nonzero gradient -> their owners' blocks
+                _ffi.check(lib.lgcn_owner_reset(ex.send.data_ptr(), ex.world, ex.blk, ex.cap, ex.req_off, ex.rcap,
+                                                ex.counts.data_ptr(), stream), "lgcn_owner_reset")
+                _ffi.check(lib.lgcn_owner_pack_rows(gu.data_ptr(), gi.data_ptr(), U, d, st.touched_rows.data_ptr(),
+                                                    st.touched_rows.numel(), st.neg.data_ptr(), B, U,
+                                                    st.c2flag.data_ptr(), st.plan.touched.data_ptr(), ex.world,
+                                                    ex.cap, ex.blk, ex.counts.data_ptr(), ex.send.data_ptr(),
+                                                    ex.overflow.data_ptr(), stream), "lgcn_owner_pack_rows")
+            elif ex is not None:
                 # this rank's rows with a possibly nonzero gradient -> the exchange slots
                 _ffi.check(lib.lgcn_rows_pack(gu.data_ptr(), gi.data_ptr(), U, d, st.touched_rows.data_ptr(),
                                               st.touched_rows.numel(), st.neg.data_ptr(), B, U,
@@ -361,8 +393,113 @@ class FusedTrainStep:
                        "lgcn_rows_accumulate")
             opt.step_rows(None, ex.ids_all, 0, first_b=ex.first)
 
+    # --- owner-sharded exchange (lgcn_amd.owner) ----------------------------------------------
+    def _owner_reduce(self) -> None:
+        """Owner side, after the blocks arrived: the received gradient rows summed per row in rank
+        order / W, and this rank's clip-norm partials over its rows of the union (row order)."""
+        ex, opt, m = self.exchange, self.optimizer, self.model
+        lib = _ffi.load()
+        stream = _ffi.stream_of(ex.ids_all.device)
+        ex.unpack()
+        n = ex.world * ex.cap
+        _ffi.check(lib.lgcn_rows_mark_first(ex.ids_all.data_ptr(), n, ex.claim.data_ptr(), ex.first.data_ptr(),
+                                            stream), "lgcn_rows_mark_first")
+        _ffi.check(lib.lgcn_rows_accumulate(ex.ids_all.data_ptr(), ex.rows_ptr(), ex.world, ex.cap, ex.blk,
+                                            ex.first.data_ptr(), opt.gu.data_ptr(), opt.gi.data_ptr(), m.num_users,
+                                            m.dim_h, float(ex.world), stream), "lgcn_rows_accumulate")
+        if opt.max_grad_norm is not None:
+            _ffi.check(lib.lgcn_rows_mark(ex.ids_all.data_ptr(), ex.first.data_ptr(), n, ex.not_union.data_ptr(), 0,
+                                          stream), "lgcn_rows_mark")
+            opt.sqnorm_partials(ex.owned, ex.not_union, ex.partials)
+            _ffi.check(lib.lgcn_rows_mark(ex.ids_all.data_ptr(), ex.first.data_ptr(), n, ex.not_union.data_ptr(), 1,
+                                          stream), "lgcn_rows_mark")
+
+    def _owner_update(self) -> None:
+        """Owner side: the Adam step on its rows of the union, then the requested rows caught up
+        to the new step and copied into the reply blocks."""
+        ex, opt, m = self.exchange, self.optimizer, self.model
+        lib = _ffi.load()
+        stream = _ffi.stream_of(ex.ids_all.device)
+        opt.step_rows_with_partials(ex.ids_all, ex.first,
+                                    ex.partials_all if opt.max_grad_norm is not None else None)
+        opt.catch_up(None, ex.req_all, 0, first_b=ex.req_valid)
+        _ffi.check(lib.lgcn_rows_gather(opt.uw.data_ptr(), opt.iw.data_ptr(), m.num_users, m.dim_h,
+                                        ex.req_all.data_ptr(), ex.req_all.numel(), ex.reply_send.data_ptr(), 0,
+                                        stream), "lgcn_rows_gather(replies)")
+
+    def _step_owner(self, st: _BatchState, nxt: _BatchState | None) -> torch.Tensor:
+        ex, opt, m = self.exchange, self.optimizer, self.model
+        lib = _ffi.load()
+        U = m.num_users
+        stream = _ffi.stream_of(m.user_embedding.weight.device)
+        if ex.pending is not st and not self._synced:
+            raise RuntimeError("OwnerExchange: this batch's rows were not fetched by the previous step (pass "
+                               "next_batch to step(), or call sync() before a step out of order)")
+        if getattr(st, "neg_step", None) != self._k:
+            self._draw(st, self._k)
+        use_graphs = self.graphs
+        if use_graphs and getattr(st, "graph", None) is not None:
+            st.graph.replay()
+            loss = st.graph_loss
+        else:
+            loss = self._lazy_grads(st, draw=False)
+            if use_graphs:
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    st.graph_loss = self._lazy_grads(st, draw=False)
+                st.graph = g
+        # the next step's rows: its batch's touched rows and its negatives, drawn now
+        ex.mine.fill_(-1)
+        if nxt is not None:
+            self._draw(nxt, self._k + 1)
+            _ffi.check(lib.lgcn_owner_pack_requests(nxt.touched_rows.data_ptr(), nxt.touched_rows.numel(),
+                                                    nxt.neg.data_ptr(), nxt.B, U, ex.world, ex.rcap, ex.blk,
+                                                    ex.req_off, ex.counts.data_ptr(), ex.send.data_ptr(),
+                                                    ex.mine.data_ptr(), ex.overflow.data_ptr(), stream),
+                       "lgcn_owner_pack_requests")
+        ex.exchange_blocks()
+        graphs_ok = use_graphs and self._owner_graphs is not None
+        if graphs_ok:
+            self._owner_graphs[0].replay()
+        else:
+            self._owner_reduce()
+        if opt.max_grad_norm is not None:
+            ex.gather_partials()
+        if graphs_ok:
+            self._owner_graphs[1].replay()
+            opt.steps += 1
+        else:
+            self._owner_update()
+        ex.exchange_replies()
+        _ffi.check(lib.lgcn_rows_gather(opt.uw.data_ptr(), opt.iw.data_ptr(), U, m.dim_h, ex.mine.data_ptr(),
+                                        ex.mine.numel(), ex.reply_recv.data_ptr(), 1, stream),
+                   "lgcn_rows_gather(scatter replies)")
+        if use_graphs and self._owner_graphs is None:
+            # the owner's two halves touch only the exchange buffers: one capture serves every batch
+            torch.cuda.synchronize()
+            steps = opt.steps
+            g0, g1 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g0):
+                self._owner_reduce()
+            with torch.cuda.graph(g1):  # records the launches only: no step runs (steps restored)
+                self._owner_update()
+            opt.steps = steps
+            self._owner_graphs = (g0, g1)
+        ex.pending = nxt
+        self._synced = False
+        self._k += 1
+        return loss
+
     def sync(self) -> None:
-        """Make the parameters current (row-lazy optimizer: replay every deferred row)."""
+        """Make the parameters current (row-lazy optimizer: replay every deferred row; owner-sharded:
+        every owner replays its rows, then one all_gather of the owned rows)."""
+        if self.owner:
+            ex, opt, m = self.exchange, self.optimizer, self.model
+            opt.catch_up(None, ex.owned, 0)
+            ex.all_gather_owned(opt.uw, opt.iw, m.num_users)
+            self._synced = True
+            return
         if self.lazy:
             self.optimizer.flush()
 
@@ -383,7 +520,18 @@ class FusedTrainStep:
 
         allreduce_grads([self.model.user_embedding.weight, self.model.item_embedding.weight], self.world)
 
-    def step(self, batch) -> torch.Tensor:
+    def step(self, batch, next_batch=None) -> torch.Tensor:
+        if self.owner:
+            st = self.state(batch.edge_index)
+            nxt = self.state(next_batch.edge_index) if next_batch is not None else None
+            if not st.lazy or (nxt is not None and not nxt.lazy):
+                raise ValueError("lazy step needs a batch whose 3B contribution ids fit int32 (3B < 2^31)")
+            return self._step_owner(st, nxt)
+        loss = self._step_replicated(batch)
+        self._k += 1
+        return loss
+
+    def _step_replicated(self, batch) -> torch.Tensor:
         if self.lazy:
             st = self.state(batch.edge_index)
             if not st.lazy:

@@ -35,6 +35,7 @@ def main():
 
     import graphs
     from lgcn_amd import cluster as C
+    from lgcn_amd import _ffi
     from lgcn_amd import distributed as D
     from lgcn_amd.optim import FusedAdam, RowLazyAdam
     from lgcn_amd.train_step import FusedTrainStep
@@ -53,27 +54,46 @@ def main():
     batches = [_Batch(torch.from_numpy(x).to(gpu)) for x in lists]
     share = D.rank_share(len(batches), world, rank, seed=0, epoch=0)
     cap = D.exchange_capacity(batches, U)
+    from lgcn_amd.owner import OwnerExchange, owner_capacity
+
+    ocap = owner_capacity(batches, U, world)
+    variants = os.environ.get("DP_VARIANTS", "dense,lazy,lazy_graphs,owner,owner_graphs").split(",")
     res = {}
-    for name in ("dense", "lazy", "lazy_graphs"):
+    clip_ = None if clip == 0 else clip
+    steps = int(os.environ.get("DP_STEPS", "12"))
+    for name in variants:
         torch.manual_seed(0)
         m = LightGCN(U, I, num_layers=3, dim_h=d).to(gpu)
+        ex = None
         if name == "dense":
-            opt = FusedAdam(m.parameters(), lr=1e-2, max_grad_norm=clip, capturable=True)
-            step = FusedTrainStep(m, opt, world=world)
+            opt = FusedAdam(m.parameters(), lr=1e-2, max_grad_norm=clip_, capturable=True)
+            step = FusedTrainStep(m, opt, world=world, neg_seed=100 + rank)
         else:
             opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-2,
-                              max_grad_norm=clip)
-            ex = D.RowExchange(cap, U + I, d, gpu, world)
-            step = FusedTrainStep(m, opt, world=world, lazy=True, exchange=ex, graphs=(name == "lazy_graphs"))
+                              max_grad_norm=clip_)
+            if name.startswith("owner"):
+                ex = OwnerExchange(ocap, U + I, d, gpu, world, rank, _ffi.load().lgcn_row_grad_norm_workspace_floats())
+            else:
+                ex = D.RowExchange(cap, U + I, d, gpu, world)
+            step = FusedTrainStep(m, opt, world=world, lazy=True, exchange=ex, graphs=name.endswith("_graphs"),
+                                  neg_seed=100 + rank)  # per-rank negatives, the same for every variant
         losses = []
-        for i in range(12):
-            torch.cuda.manual_seed(100 + 10 * i + rank)  # per-rank negatives, same for every variant
-            losses.append(step.step(batches[share[i % len(share)]]).item())
+        for i in range(steps):
+            b = batches[share[i % len(share)]]
+            if name.startswith("owner"):
+                nxt = batches[share[(i + 1) % len(share)]] if i + 1 < steps else None
+                losses.append(step.step(b, nxt).item())
+            else:
+                losses.append(step.step(b).item())
         step.sync()
         torch.cuda.synchronize()
+        if name.startswith("owner"):
+            ex.check_overflow()
         res[name] = {"losses": losses, "user": m.user_embedding.weight.detach().cpu(),
-                     "item": m.item_embedding.weight.detach().cpu()}
+                     "item": m.item_embedding.weight.detach().cpu(),
+                     "bytes_per_step": (ex.bytes / steps) if ex is not None and hasattr(ex, "bytes") else None}
     res["cap"] = cap
+    res["ocap"] = ocap
     res["d"] = d
     torch.save(res, out)
     dist.barrier()

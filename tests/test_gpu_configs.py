@@ -144,9 +144,9 @@ def _free_port():
 
 
 def test_c4_dp2_exchange_on_c3_batches(gpu, c3, tmp_path):
-    """C4 rehearsal: two ranks (gloo, one GPU) train C3 batches at K=3 d=128 three ways; the
-    row-sparse exchange (eager and hipGraph) is bitwise the dense all_reduce + FusedAdam step
-    without clipping, and both ranks end bitwise identical."""
+    """C4 rehearsal: two ranks (gloo, one GPU) train C3 batches at K=3 d=128 five ways; the
+    row-sparse exchange and the owner-sharded optimizer (each eager and hipGraph) are bitwise the
+    dense all_reduce + FusedAdam step without clipping, and both ranks end bitwise identical."""
     port = str(_free_port())
     worker = str(ROOT / "tests" / "dp_exchange_worker.py")
     outs = [str(tmp_path / f"r{r}.pt") for r in range(2)]
@@ -156,7 +156,7 @@ def test_c4_dp2_exchange_on_c3_batches(gpu, c3, tmp_path):
     logs = []
     for p in procs:
         try:
-            logs.append(p.communicate(timeout=110)[0])
+            logs.append(p.communicate(timeout=200)[0])
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
@@ -170,9 +170,13 @@ def test_c4_dp2_exchange_on_c3_batches(gpu, c3, tmp_path):
         assert torch.equal(res[0][name]["item"], res[1][name]["item"]), name
     for r in range(2):
         dn, lz, lg = res[r]["dense"], res[r]["lazy"], res[r]["lazy_graphs"]
-        assert dn["losses"] == lz["losses"] == lg["losses"]
+        ow, og = res[r]["owner"], res[r]["owner_graphs"]
+        assert dn["losses"] == lz["losses"] == lg["losses"] == ow["losses"] == og["losses"]
         for k in ("user", "item"):
             assert torch.equal(dn[k], lz[k]) and torch.equal(lz[k], lg[k]), k
+            assert torch.equal(lz[k], ow[k]) and torch.equal(ow[k], og[k]), k
+    print(f"C4 rehearsal (W=2, C3 batches, d=128) bytes received per rank per step: replicated "
+          f"{res[0]['lazy']['bytes_per_step'] / 1e6:.2f} MB, owner-sharded {res[0]['owner']['bytes_per_step'] / 1e6:.2f} MB")
 
 
 C5_SCALE = 40

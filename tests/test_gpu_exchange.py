@@ -172,9 +172,11 @@ def test_dp2_row_exchange_matches_dense_allreduce(gpu, tmp_path, clip):
     for p, log in zip(procs, logs):
         assert p.returncode == 0, log
     res = [torch.load(o, weights_only=True) for o in outs]
-    for name in ("dense", "lazy", "lazy_graphs"):
+    for name in ("dense", "lazy", "lazy_graphs", "owner", "owner_graphs"):
         assert torch.equal(res[0][name]["user"], res[1][name]["user"]), name
         assert torch.equal(res[0][name]["item"], res[1][name]["item"]), name
+    for r in range(2):
+        _check_owner_vs_replicated(res[r], clip)
     for r in range(2):
         d, lz, lg = res[r]["dense"], res[r]["lazy"], res[r]["lazy_graphs"]
         assert lz["losses"] == lg["losses"]
@@ -187,3 +189,58 @@ def test_dp2_row_exchange_matches_dense_allreduce(gpu, tmp_path, clip):
                 assert abs(a - b) <= 1e-5 * max(1.0, abs(a))
             for k in ("user", "item"):
                 assert (d[k] - lz[k]).abs().max().item() <= 1e-3 * d[k].abs().max().item()
+
+
+def _check_owner_vs_replicated(res, clip):
+    """Owner-sharded exchange vs the replicated one (both row-lazy): bitwise whenever the clip
+    coefficient is exactly 1 (the same rank-ordered sums, the same updates and replays); with an
+    active clip the two norms sum the same squares in another order (losses to 1e-5)."""
+    lz, ow, og = res["lazy"], res["owner"], res["owner_graphs"]
+    assert ow["losses"] == og["losses"]
+    assert torch.equal(ow["user"], og["user"]) and torch.equal(ow["item"], og["item"])
+    if clip == float("inf"):
+        assert ow["losses"] == lz["losses"]
+        assert torch.equal(ow["user"], lz["user"]) and torch.equal(ow["item"], lz["item"])
+    else:
+        for a, b in zip(lz["losses"], ow["losses"]):
+            assert abs(a - b) <= 1e-5 * max(1.0, abs(a))
+
+
+def _spawn(world, tmp_path, clip, variants, steps=12, npz=None, timeout=300):
+    port = str(_free_port())
+    worker = str(ROOT / "tests" / "dp_exchange_worker.py")
+    outs = [str(tmp_path / f"w{world}_r{r}.pt") for r in range(world)]
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", DP_VARIANTS=variants, DP_STEPS=str(steps),
+               OMP_NUM_THREADS="1")
+    extra = [npz] if npz else []
+    procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), str(world), port, outs[r], str(clip), *extra],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(world)]
+    logs = []
+    try:
+        for p in procs:
+            logs.append(p.communicate(timeout=timeout)[0])
+    except subprocess.TimeoutExpired:
+        for q in procs:
+            q.kill()
+        raise
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    return [torch.load(o, weights_only=True) for o in outs]
+
+
+@pytest.mark.parametrize("clip", [float("inf"), 1.0])
+def test_dp8_owner_exchange_matches_replicated(gpu, tmp_path, clip):
+    """Eight ranks (gloo, one GPU), 16 steps with a different next batch each step: the
+    owner-sharded optimizer (lgcn_amd.owner; gradient rows to their owners, rows fetched for the
+    next step) == the replicated row exchange, bitwise without clipping; every rank ends with
+    bitwise identical tables after sync(); the bytes each rank receives per step are printed."""
+    res = _spawn(8, tmp_path, clip, "lazy,owner,owner_graphs", steps=16)
+    for name in ("lazy", "owner", "owner_graphs"):
+        for r in range(1, 8):
+            assert torch.equal(res[0][name]["user"], res[r][name]["user"]), (name, r)
+            assert torch.equal(res[0][name]["item"], res[r][name]["item"]), (name, r)
+    for r in range(8):
+        _check_owner_vs_replicated(res[r], clip)
+    print(f"W=8 bytes received per rank per step: replicated {res[0]['lazy']['bytes_per_step'] / 1e6:.3f} MB, "
+          f"owner {res[0]['owner']['bytes_per_step'] / 1e6:.3f} MB (cap {res[0]['cap']}, owner cap {res[0]['ocap']})")
