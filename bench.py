@@ -342,7 +342,7 @@ def main():
     ap.add_argument("--shard", default=None,
                     help="c2, N > 1: RxF grid (R row groups x F column groups, R*F = N); default: every "
                          "lgcn_amd.sharded.grid_candidates grid is timed for a few steps and the fastest runs")
-    ap.add_argument("--exchange-mode", choices=["allgather", "p2p"], default="allgather",
+    ap.add_argument("--exchange-mode", choices=["allgather", "p2p", "reduce"], default="allgather",
                     help="c2 with --shard and R > 1: one all_gather per block, or sends to every peer")
     ap.add_argument("--workload", choices=["propagate", "train"], default="propagate",
                     help="propagate: C2 headline (default); train: C3/C4 Cluster-GCN training steps")
@@ -424,7 +424,8 @@ def main():
     exchange = None
     grid_trials = None
     if sharded:
-        from lgcn_amd.sharded import (BlockExchange, RowShards, ShardedPlan, ShardGrid, grid_candidates,
+        from lgcn_amd.sharded import (BlockExchange, ItemReducer, ReducePlan, RowShards, ShardedPlan, ShardGrid,
+                                      UserShards, grid_candidates, propagate_forward_reduced,
                                       propagate_forward_sharded)
 
         in_deg = np.bincount(graph.edge_index[1], minlength=N)
@@ -442,11 +443,19 @@ def main():
                 uw_c, iw_c = user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous()
                 return dict(grid=grid, shards=None, splan=None, scheds=[cplan.schedule("fwd", c1 - c0)], ex=None,
                             mode=None, step=lambda: lgcn_amd.propagate_forward(uw_c, iw_c, cplan, K))
+            if (grid.R, grid.F) not in groups:  # collective: every rank creates the column groups
+                groups[(grid.R, grid.F)] = grid.exchange_group(dist)
+            if mode == "reduce":
+                # users sharded, item rows all-reduced per layer (lgcn_amd.sharded.ReducePlan)
+                ushards = UserShards.build(in_deg, U, grid.R)
+                rplan = ReducePlan(ei, ushards, grid.row_group, c1 - c0, chunk)
+                red = ItemReducer(grid.R, groups[(grid.R, grid.F)])
+                x0u, x0i = user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous()
+                return dict(grid=grid, shards=ushards, splan=rplan, scheds=[rplan.users, rplan.partial], ex=red,
+                            mode=mode, step=lambda: propagate_forward_reduced(x0u, x0i, rplan, K, red))
             shards = RowShards.build(in_deg, U, grid.R)
             splan = ShardedPlan(ei, shards, grid.row_group, c1 - c0, chunk)
             x0p = shards.to_padded(user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous())
-            if (grid.R, grid.F) not in groups:  # collective: every rank creates the column groups
-                groups[(grid.R, grid.F)] = grid.exchange_group(dist)
             ex = (BlockExchange(shards, grid.row_group, groups[(grid.R, grid.F)], grid.members, mode or "allgather")
                   if grid.R > 1 else None)
             return dict(grid=grid, shards=shards, splan=splan, scheds=[h.direction for h in splan.halves], ex=ex,
@@ -511,6 +520,10 @@ def main():
         if shards is None:
             log(f"[rank {rank}] grid {grid.R}x{grid.F}: all rows, columns [{c0}, {c1}) with the one-GPU plan at "
                 f"width {d}, {time.perf_counter() - t0:.2f} s")
+        elif st["mode"] == "reduce":
+            ua, ub_ = shards.users(g_r)
+            log(f"[rank {rank}] grid {grid.R}x{grid.F} reduce: row group {g_r} (users {ub_ - ua} of {U}, all {I} "
+                f"items from {splan.n_sub} edges), columns [{c0}, {c1}), {time.perf_counter() - t0:.2f} s")
         else:
             ua, ub_ = shards.user_rows(g_r)
             ia, ib_ = shards.item_rows(g_r)
@@ -609,7 +622,14 @@ def main():
                                        f"offset {synth.ML25M_USER_OFFSET})"),
                    "parallelism": (f"feature-sharded over {world} GPU(s): {d} columns each, full plan per rank, "
                                    "no collective") if c5 else
-                                  (f"{grid.R} row groups x {grid.F} column groups over {world} GPUs: each rank "
+                                  (f"{grid.R} row groups x {grid.F} column groups over {world} GPUs (reduce): each "
+                                   f"rank propagates {d} of {d_full} columns of one edge-balanced user range and "
+                                   f"the partial sums of every item row over the edges its users source; the item "
+                                   f"partials are all-reduced within the column group once per layer "
+                                   f"({args.dist_backend}, overlapped with the user pass and the next partial pass); "
+                                   f"column groups exchange nothing; within 1e-5 per row of the 1-GPU result"
+                                   if sharded and st["mode"] == "reduce" else
+                                   f"{grid.R} row groups x {grid.F} column groups over {world} GPUs: each rank "
                                    f"propagates {d} of {d_full} columns of one edge-balanced destination row range "
                                    f"(whole graph and whole column share of the table on every rank); " +
                                    (f"ranks of a column group exchange each exchanged layer's two row blocks "
@@ -637,8 +657,12 @@ def main():
     if grid_trials is not None:
         result["config"]["grid_trials_ms_per_step"] = grid_trials
     if exchange is not None:
-        result["exchange"] = {"mode": exchange.mode, "block_exchanges_per_step": 2 * (K - 1),
-                              "MB_received_per_rank_per_step": exchange.bytes / args.steps / 1e6}
+        if st["mode"] == "reduce":
+            result["exchange"] = {"mode": "reduce", "all_reduces_per_step": K,
+                                  "MB_received_per_rank_per_step": exchange.bytes / args.steps / 1e6}
+        else:
+            result["exchange"] = {"mode": exchange.mode, "block_exchanges_per_step": 2 * (K - 1),
+                                  "MB_received_per_rank_per_step": exchange.bytes / args.steps / 1e6}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if c5:
             # C5 does not fit a CPU run: the same generator at 1/100 scale (5e6 edges), K and d of C5

@@ -286,6 +286,18 @@ int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split,
                    const int64_t* u, const int64_t* p, const int64_t* n, int64_t B, int32_t d,
                    const uint8_t* touched, float div, float mul,
                    float coeff, float* cf, float* cw, float* terms, lgcn_stream_t stream);
+/* Column-sharded form (exact single-GPU training split over ranks by embedding columns, SURVEY
+ * §8e's parity-preserving alternative): the rows are one rank's d of d_full columns.
+ *   phase 1: sums[b*6 + k] = this rank's partial of (|u|^2, |p|^2, |n|^2, u.p, u.n, reg squares)
+ *            over its columns; nothing else is written;
+ *   (the caller all-reduces sums over the column groups)
+ *   phase 2: reads the six full sums and writes cf / cw / terms as lgcn_bpr_fused does, for this
+ *            rank's columns; the reg scale uses d_full (cw rows = coeff * 2 / (B * d_full) * W).
+ * d in {8, 16, ..., 512}. Replaces the same reference code as lgcn_bpr_fused. */
+int lgcn_bpr_fused_cols(const float* f_lo, const float* f_hi, int64_t f_split, const float* w_lo, const float* w_hi,
+                        int64_t w_split, int64_t U, const int64_t* u, const int64_t* p, const int64_t* n, int64_t B,
+                        int32_t d, int32_t d_full, const uint8_t* touched, float div, float mul, float coeff, float* sums,
+                        int32_t phase, float* cf, float* cw, float* terms, lgcn_stream_t stream);
 /* partial: NULL, or float[2 * LGCN_LOSS_PARTS] scratch — large batches then sum in two stages
  * (LGCN_LOSS_PARTS blocks over contiguous shares, one block over the shares): a fixed association
  * either way, so the loss is deterministic. */

@@ -87,9 +87,17 @@ struct BprArgs {
     float* cf;     // [3B, d] dF rows (u | p | n)
     float* cw;     // [3B, d] reg-gradient rows for W (u | p | n)
     float* terms;  // [2B]: softplus terms | reg row sums
+    // column-sharded training (lgcn_bpr_fused_cols): the rows are one rank's d of d_full columns
+    float* sums;     // [B, 6] per-triplet (|u|^2, |p|^2, |n|^2, u.p, u.n, reg squares)
+    int32_t d_full;  // the full width (reg mean); == d unsharded
 };
 
-template <int LPR, int NV>
+// phase 0: fused (the sums reduced inside the lane group); 1: write this rank's column partials
+// of the six sums to a.sums and stop; 2: read the six full sums from a.sums (all-reduced over the
+// column groups) and finish with them.
+constexpr int kBprFused = 0, kBprPartials = 1, kBprFromSums = 2;
+
+template <int LPR, int NV, int PHASE>
 __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
     constexpr int GPB = kBlock / LPR;
     const int g = threadIdx.x / LPR;
@@ -136,6 +144,17 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
     sup = group_sum<LPR>(sup);
     sun = group_sum<LPR>(sun);
     sreg = group_sum<LPR>(sreg);
+    if constexpr (PHASE == kBprPartials) {
+        if (l == 0) {
+            float* o = a.sums + b * 6;
+            o[0] = suu, o[1] = spp, o[2] = snn, o[3] = sup, o[4] = sun, o[5] = sreg;
+        }
+        return;
+    }
+    if constexpr (PHASE == kBprFromSums) {
+        const float* o = a.sums + b * 6;
+        suu = o[0], spp = o[1], snn = o[2], sup = o[3], sun = o[4], sreg = o[5];
+    }
     const float nu = sqrtf(suu), np = sqrtf(spp), nn = sqrtf(snn);
     const float cp = sup / (nu * np);
     const float cn = sun / (nu * nn);
@@ -146,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
     const float inv_b = 1.0f / static_cast<float>(a.B);
     const float dcp = -sg * inv_b;  // d loss / d cos(u,p)
     const float dcn = sg * inv_b;   // d loss / d cos(u,n)
-    const float kreg = a.coeff * 2.0f / (static_cast<float>(a.B) * static_cast<float>(a.d));
+    const float kreg = a.coeff * 2.0f / (static_cast<float>(a.B) * static_cast<float>(a.d_full));
     const float inu = 1.0f / nu, inp = 1.0f / np, inn = 1.0f / nn;
     float4* cfu = reinterpret_cast<float4*>(a.cf + b * d) + l;
     float4* cfp = reinterpret_cast<float4*>(a.cf + (a.B + b) * d) + l;
@@ -643,11 +662,29 @@ int launch_fra(const int64_t* keys, int64_t B, int64_t key_offset, const float* 
 }
 
 template <int LPR, int NV>
-int launch_bpr(const BprArgs& a, hipStream_t s) {
+int launch_bpr(const BprArgs& a, int phase, hipStream_t s) {
     constexpr int GPB = kBlock / LPR;
     const int64_t blocks = (a.B + GPB - 1) / GPB;
-    if (blocks > 0) k_bpr_fused<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
+    if (blocks > 0) {
+        const dim3 grid(static_cast<unsigned>(blocks));
+        if (phase == kBprPartials) k_bpr_fused<LPR, NV, kBprPartials><<<grid, kBlock, 0, s>>>(a);
+        else if (phase == kBprFromSums) k_bpr_fused<LPR, NV, kBprFromSums><<<grid, kBlock, 0, s>>>(a);
+        else k_bpr_fused<LPR, NV, kBprFused><<<grid, kBlock, 0, s>>>(a);
+    }
     return check_launch("k_bpr_fused");
+}
+
+int bpr_dispatch(const BprArgs& a, int phase, hipStream_t s) {
+    switch (a.d) {
+        case 8: return launch_bpr<2, 1>(a, phase, s);
+        case 16: return launch_bpr<4, 1>(a, phase, s);
+        case 32: return launch_bpr<8, 1>(a, phase, s);
+        case 64: return launch_bpr<16, 1>(a, phase, s);
+        case 128: return launch_bpr<32, 1>(a, phase, s);
+        case 256: return launch_bpr<64, 1>(a, phase, s);
+        case 512: return launch_bpr<64, 2>(a, phase, s);
+        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_bpr_fused: d=%d (supported 8..512, powers of two)", a.d);
+    }
 }
 
 template <int LPR, int NV>
@@ -677,17 +714,26 @@ int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split, const 
     if (d % 4 != 0 || !al16(f_lo) || !al16(w_lo) || (f_hi && !al16(f_hi)) || (w_hi && !al16(w_hi)) || !al16(cf) ||
         (cw && !al16(cw)))
         return fail(LGCN_E_UNSUPPORTED, "lgcn_bpr_fused: needs d %% 4 == 0 and 16-byte aligned rows (d=%d)", d);
-    BprArgs a{f_lo, f_hi, f_split, w_lo, w_hi, w_split, U, u, p, n, B, d, touched, div, mul, coeff, cf, cw, terms};
-    hipStream_t s = as_stream(stream);
-    switch (d) {
-        case 16: return launch_bpr<4, 1>(a, s);
-        case 32: return launch_bpr<8, 1>(a, s);
-        case 64: return launch_bpr<16, 1>(a, s);
-        case 128: return launch_bpr<32, 1>(a, s);
-        case 256: return launch_bpr<64, 1>(a, s);
-        case 512: return launch_bpr<64, 2>(a, s);
-        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_bpr_fused: d=%d (supported 16..512, powers of two)", d);
-    }
+    BprArgs a{f_lo, f_hi, f_split, w_lo, w_hi, w_split, U, u, p, n, B, d, touched, div, mul, coeff, cf, cw, terms,
+              nullptr, d};
+    return bpr_dispatch(a, kBprFused, as_stream(stream));
+}
+
+int lgcn_bpr_fused_cols(const float* f_lo, const float* f_hi, int64_t f_split, const float* w_lo, const float* w_hi,
+                        int64_t w_split, int64_t U, const int64_t* u, const int64_t* p, const int64_t* n, int64_t B,
+                        int32_t d, int32_t d_full, const uint8_t* touched, float div, float mul, float coeff, float* sums,
+                        int32_t phase, float* cf, float* cw, float* terms, lgcn_stream_t stream) {
+    if (B < 0 || d <= 0 || d_full < d || U < 0 || (phase != kBprPartials && phase != kBprFromSums))
+        return fail(LGCN_E_ARG, "lgcn_bpr_fused_cols: bad sizes or phase");
+    if (B == 0) return LGCN_OK;
+    if (!f_lo || !w_lo || !u || !p || !n || !sums || (phase == kBprFromSums && (!cf || !terms)))
+        return fail(LGCN_E_ARG, "lgcn_bpr_fused_cols: null pointer");
+    if (d % 4 != 0 || !al16(f_lo) || !al16(w_lo) || (f_hi && !al16(f_hi)) || (w_hi && !al16(w_hi)) ||
+        (cf && !al16(cf)) || (cw && !al16(cw)))
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_bpr_fused_cols: needs d %% 4 == 0 and 16-byte aligned rows (d=%d)", d);
+    BprArgs a{f_lo, f_hi, f_split, w_lo, w_hi, w_split, U, u, p, n, B, d, touched, div, mul, coeff, cf, cw, terms,
+              sums, d_full};
+    return bpr_dispatch(a, phase, as_stream(stream));
 }
 
 int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
@@ -710,6 +756,7 @@ int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_
     const RegSrc reg{reg_w_lo, reg_w_hi, reg_w_split, reg_coeff, reg_B};
 #define LGCN_RS(L, V) launch_rs<L, V>(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg, c2buf, c2flag, overflow, store_unless, s)
     switch (d) {
+        case 8: return LGCN_RS(2, 1);
         case 16: return LGCN_RS(4, 1);
         case 32: return LGCN_RS(8, 1);
         case 64: return LGCN_RS(16, 1);
@@ -738,6 +785,7 @@ int lgcn_sorted_scatter_add(const int64_t* rowptr, const int32_t* perm, int64_t 
     const RegSrc reg{reg_w_lo, reg_w_hi, reg_w_split, reg_coeff, reg_B};
 #define LGCN_SS(L, V) launch_ss<L, V>(rowptr, perm, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg, c2buf, c2flag, store_unless, s)
     switch (d) {
+        case 8: return LGCN_SS(2, 1);
         case 16: return LGCN_SS(4, 1);
         case 32: return LGCN_SS(8, 1);
         case 64: return LGCN_SS(16, 1);
@@ -760,6 +808,7 @@ int lgcn_reg_rows_add(const int64_t* rowptr, const int32_t* rows, int64_t n_rows
     hipStream_t s = as_stream(stream);
     const RegSrc reg{w_lo, w_hi, w_split, coeff, B};
     switch (d) {
+        case 8: return launch_reg<2, 1>(rowptr, rows, n_rows, reg, d, out_lo, out_hi, split, s);
         case 16: return launch_reg<4, 1>(rowptr, rows, n_rows, reg, d, out_lo, out_hi, split, s);
         case 32: return launch_reg<8, 1>(rowptr, rows, n_rows, reg, d, out_lo, out_hi, split, s);
         case 64: return launch_reg<16, 1>(rowptr, rows, n_rows, reg, d, out_lo, out_hi, split, s);
@@ -777,6 +826,7 @@ int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, co
     hipStream_t s = as_stream(stream);
 #define LGCN_FRA(L, V) launch_fra<L, V>(keys, B, key_offset, c2buf, c2flag, d, out_lo, out_hi, split, s)
     switch (d) {
+        case 8: return LGCN_FRA(2, 1);
         case 16: return LGCN_FRA(4, 1);
         case 32: return LGCN_FRA(8, 1);
         case 64: return LGCN_FRA(16, 1);
@@ -813,6 +863,7 @@ int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C
         return fail(LGCN_E_UNSUPPORTED, "lgcn_segment_rows: needs d %% 4 == 0 and aligned rows");
     hipStream_t s = as_stream(stream);
     switch (d) {
+        case 8: return launch_seg<2, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, mul, div, s);
         case 16: return launch_seg<4, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, mul, div, s);
         case 32: return launch_seg<8, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, mul, div, s);
         case 64: return launch_seg<16, 1>(rowptr, perm, C, N, d, out_lo, out_hi, split, add, mul, div, s);

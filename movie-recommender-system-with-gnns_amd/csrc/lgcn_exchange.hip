@@ -236,6 +236,7 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 #define LGCN_EX_DISPATCH(CALL, WHAT)                                              \
     switch (d) {                                                                  \
+        case 8: CALL(2, 1); break;                                                \
         case 16: CALL(4, 1); break;                                               \
         case 32: CALL(8, 1); break;                                               \
         case 64: CALL(16, 1); break;                                              \

@@ -271,6 +271,7 @@ int check_tables(const RowTables& T, bool need_grad) {
 
 #define LGCN_ROW_DISPATCH(CALL)                                                     \
     switch (T.d) {                                                                  \
+        case 8: return CALL(2, 1);                                                  \
         case 16: return CALL(4, 1);                                                 \
         case 32: return CALL(8, 1);                                                 \
         case 64: return CALL(16, 1);                                                \

@@ -189,14 +189,34 @@ class RowLazyAdam:
         self.steps += 1
 
     def step_rows(self, rows_a: torch.Tensor | None, keys_b: torch.Tensor | None = None, off_b: int = 0,
-                  first_b: torch.Tensor | None = None, skip_b: torch.Tensor | None = None) -> None:
+                  first_b: torch.Tensor | None = None, skip_b: torch.Tensor | None = None,
+                  gather_partials=None) -> None:
         """One Adam step whose gradient (self.gu / self.gi) is zero outside the listed rows, which
         must be duplicate-free (first_b / skip_b filter list b): clip norm over them, then the
-        update; rows not listed are deferred."""
+        update; rows not listed are deferred. gather_partials (column-sharded training: each rank
+        holds some columns of every row): called with this rank's norm block partials, returns
+        every rank's partials in rank order — the norm is finished over all of them."""
         if self.steps + 1 > self.max_steps:
             raise RuntimeError(f"RowLazyAdam: more than max_steps={self.max_steps} steps")
         lib = _ffi.load()
         clip = None
+        if self.max_grad_norm is not None and gather_partials is not None:
+            na = rows_a.numel() if rows_a is not None else 0
+            nb = keys_b.numel() if keys_b is not None else 0
+            if getattr(self, "_partials", None) is None:
+                self._partials = torch.empty(lib.lgcn_row_grad_norm_workspace_floats(), dtype=torch.float32,
+                                             device=self.device)
+            _ffi.check(lib.lgcn_row_grad_sqnorm(self.gu.data_ptr(), self.gi.data_ptr(), self.U, self.d,
+                                                _ffi.ptr(rows_a), na, _ffi.ptr(keys_b), nb, off_b, _ffi.ptr(first_b),
+                                                _ffi.ptr(skip_b), self._partials.data_ptr(),
+                                                _ffi.stream_of(self.device)), "lgcn_row_grad_sqnorm")
+            every = gather_partials(self._partials)
+            _ffi.check(lib.lgcn_row_grad_norm_finish(every.data_ptr(), every.numel(), float(self.max_grad_norm),
+                                                     self.last_norm.data_ptr(), self.step_dev.data_ptr(),
+                                                     _ffi.stream_of(self.device)), "lgcn_row_grad_norm_finish")
+            self._row_adam(rows_a, keys_b, off_b, first_b, skip_b, 0, self.last_norm, 3)
+            self.steps += 1
+            return
         if self.max_grad_norm is not None:
             na = rows_a.numel() if rows_a is not None else 0
             nb = keys_b.numel() if keys_b is not None else 0

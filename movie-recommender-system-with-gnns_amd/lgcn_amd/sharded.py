@@ -167,8 +167,9 @@ def grid_shape(world: int, d: int) -> tuple[int, int]:
     return world, 1
 
 
-def grid_candidates(world: int, d: int) -> list[tuple[int, int, str | None]]:
-    """(R, F, exchange mode) grids bench.py times before it picks one for a world of ranks: every
+def grid_candidates(world: int, d: int, bipartite: bool = True) -> list[tuple[int, int, str | None]]:
+    """(R, F, exchange mode) grids bench.py times before it picks one for a world of ranks (mode
+    "reduce" — users sharded, item rows all-reduced — for every R > 1 of a bipartite graph): every
     column split F | world with d / F a multiple of 4 and >= 8; the rows-only grid (F = 1) when no
     column split exists or when world >= 4 — it moves the most bytes in total, but over R - 1 links
     at once, so its bytes per xGMI link match the column-split grids' (C2 at N = 8: ~14 MB per link
@@ -184,6 +185,8 @@ def grid_candidates(world: int, d: int) -> list[tuple[int, int, str | None]]:
             out.append((R, F, None))
         else:
             out += [(R, F, m) for m in (EXCHANGE_MODES if R >= 3 else EXCHANGE_MODES[:1])]
+            if bipartite:  # users sharded, item rows all-reduced (ReducePlan)
+                out.append((R, F, "reduce"))
     if any(F > 1 for _, F, _ in out) and world < 4:
         out = [c for c in out if c[1] > 1]
     return out
@@ -464,3 +467,222 @@ def propagate_forward_sharded(x0p: torch.Tensor, splan, K: int, exchange: BlockE
                     started[b] = exchange.start(dst, b)
         pending = started
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# "reduce" row groups: users sharded, item rows reduced (bipartite graphs)
+# ---------------------------------------------------------------------------------------------
+#
+# The all_gather grid above moves every exchanged layer's whole output (users AND items, 57 MB per
+# layer at C2 d = 64) to every rank of a column group. On a bipartite graph the item side is the
+# small one (I = 59k of N = 222k at C2), and user rows only ever gather item rows. So:
+#
+# * row group g owns one edge-balanced range of USER rows; every rank holds every ITEM row;
+# * user rows of layer k: the rank's own users, summed over all their in-edges (sources are items)
+#   — the one-GPU plain schedule's rows, from the full item table of layer k-1;
+# * item rows of layer k: each rank sums, for EVERY item, the in-edges whose source user it owns
+#   (a CSR of that edge subset with the whole graph's gcn_norm weights); the R partial tables are
+#   summed by one all_reduce per layer (RCCL, on a side stream, overlapped with the other half and
+#   the next layer's partial pass), then the LightGCN epilogue runs on the reduced item rows
+#   (an identity pass through lgcn_spmm: weight-1 self edges, so it is the same epilogue code).
+#
+# Exchange per rank per K-layer step: K all_reduces of I x d/F floats (a ring moves 2 (R-1)/R of
+# it), instead of K-1 all_gathers of (R-1)/R of N x d/F. C2 at 8 x 1: 3 x 26.4 MB vs 2 x 52 MB;
+# and a rank's item partials gather only its own 1/R of the user table (cache-resident).
+# Numerics: a user row is one sequential chain as on one GPU; an item row is the sum of R partial
+# chains (its users cut into R ranges), i.e. reassociated like a chunked hub row: within 1e-5.
+
+
+@dataclasses.dataclass
+class UserShards:
+    """Edge-balanced user-row ranges of R row groups (items replicated)."""
+
+    R: int
+    U: int
+    I: int
+    ub: np.ndarray  # int64[R+1]
+
+    @classmethod
+    def build(cls, in_degree: np.ndarray, U: int, R: int) -> "UserShards":
+        deg = np.asarray(in_degree, dtype=np.int64)
+        if U < 0 or deg.size < U or R < 1:
+            raise ValueError(f"bad shard request U={U} N={deg.size} R={R}")
+        return cls(R, U, deg.size - U, balanced_bounds(deg[:U] + ROW_COST, R))
+
+    @property
+    def N(self) -> int:
+        return self.U + self.I
+
+    def users(self, g: int) -> tuple[int, int]:
+        return int(self.ub[g]), int(self.ub[g + 1])
+
+
+def _identity_items(U: int, N: int, dev, chunk: int, stream) -> object:
+    """The plain schedule of weight-1 self edges on the item rows (the item epilogue pass)."""
+    from .plan import CsrDirection, _schedule
+
+    I = N - U
+    rowptr = torch.cat([torch.zeros(U, dtype=torch.int64), torch.arange(I + 1, dtype=torch.int64)]).to(dev)
+    col = torch.arange(U, N, dtype=torch.int32, device=dev)
+    eid = torch.arange(I, dtype=torch.int32, device=dev)
+    val = torch.ones(I, dtype=torch.float32, device=dev)
+    mask = torch.zeros(N, dtype=torch.uint8, device=dev)
+    mask[U:] = 1
+    return CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, I, chunk, U, mask, stream), chunk)
+
+
+class ReducePlan:
+    """Row group g's plans for the reduce mode (see above): its users' rows over the whole CSR, the
+    item partials over the edges its users source, and the item epilogue pass."""
+
+    def __init__(self, edge_index: torch.Tensor, shards: UserShards, g: int, d: int, chunk: int | None = None):
+        from .plan import DEFAULT_CHUNK, CsrDirection, _build_direction, _schedule
+
+        _ffi.require_device(edge_index, "ReducePlan")
+        if edge_index.dim() != 2 or edge_index.shape[0] != 2 or edge_index.dtype != torch.int64:
+            raise ValueError("edge_index must be int64 [2, E]")
+        self.shards, self.g, self.d = shards, int(g), int(d)
+        self.chunk = rank_chunk(int(chunk or DEFAULT_CHUNK), max(shards.R, 2))
+        dev = edge_index.device
+        N, U = shards.N, shards.U
+        E = int(edge_index.shape[1])
+        if E and (int(edge_index.min()) < 0 or int(edge_index.max()) >= N):
+            raise IndexError(f"edge_index holds node ids outside [0, {N})")
+        src, dst = edge_index[0].contiguous(), edge_index[1].contiguous()
+        if E and not bool(((src < U) != (dst < U)).all().item()):
+            raise ValueError("the reduce mode needs a bipartite user-item graph")
+        stream = _ffi.stream_of(dev)
+        ua, ub = shards.users(self.g)
+        own = torch.zeros(N, dtype=torch.uint8, device=dev)
+        own[ua:ub] = 1
+        # the whole graph's CSR (its in-degrees give gcn_norm), scheduled on this group's users
+        self.users, self.dis, bad = _build_direction(dst, src, N, self.chunk, U, None, stream, own)
+        if bad:
+            raise IndexError(f"edge_index holds {bad} edge(s) with a node id outside [0, {N})")
+        self.users.block_split = False
+        # the item partials: the edges whose source is one of this group's users, every item row
+        # scheduled (0 where none), weights from the whole graph's degrees
+        sel = (src >= ua) & (src < ub)
+        items = torch.zeros(N, dtype=torch.uint8, device=dev)
+        items[U:] = 1
+        self.partial, _, _ = _build_direction(dst[sel].contiguous(), src[sel].contiguous(), N, self.chunk, U,
+                                              self.dis, stream, items)
+        self.partial.block_split = False
+        self.identity = _identity_items(U, N, dev, self.chunk, stream)
+        self.n_sub = int(sel.sum().item())
+        self.scratch = {}
+
+    def _part(self, direction, d):
+        key = (id(direction), d)
+        if direction.n_partials and key not in self.scratch:
+            self.scratch[key] = torch.empty((direction.n_partials, d), dtype=torch.float32,
+                                            device=direction.rowptr.device)
+        return self.scratch.get(key)
+
+    # the three kinds of pass; tables are (lo, hi, split = U) split tables
+    def run_partial(self, x_users: torch.Tensor, part_items: torch.Tensor) -> None:
+        from .propagate import spmm
+
+        N, U = self.shards.N, self.shards.U
+        spmm(self.partial, N, self.d, (x_users, part_items, U), None, (part_items, part_items, U), None,
+             _ffi.EPI_STORE, 1.0, 1.0, self._part(self.partial, self.d))
+
+    def run_users(self, x_items: torch.Tensor, e, acc, y, mode: int, div: float, mul: float) -> None:
+        from .propagate import spmm
+
+        N, U = self.shards.N, self.shards.U
+        spmm(self.users, N, self.d, (x_items, x_items, U), e, acc, y, mode, div, mul, self._part(self.users, self.d))
+
+    def run_item_epilogue(self, v_items: torch.Tensor, e, acc, mode: int, div: float, mul: float) -> None:
+        from .propagate import spmm
+
+        N, U = self.shards.N, self.shards.U
+        spmm(self.identity, N, self.d, (v_items, v_items, U), e, acc, None, mode, div, mul, None)
+
+
+class ItemReducer:
+    """Sum of the R item-partial tables of a column group: one all_reduce per layer (nccl: RCCL on
+    a side stream after an event on the compute stream, waited on before the rows are read; gloo:
+    synchronous, through host memory)."""
+
+    def __init__(self, R: int, group=None):
+        import torch.distributed as dist
+
+        self.dist, self.R, self.group = dist, int(R), group
+        self.nccl = R > 1 and dist.get_backend(group) == "nccl"
+        self.stream = None
+        self.bytes = 0  # ring all_reduce traffic received per rank over the run
+
+    def start(self, buf: torch.Tensor):
+        self.bytes += int(2 * (self.R - 1) / self.R * buf.numel() * buf.element_size())
+        if self.R == 1:
+            return None
+        if self.nccl:
+            if self.stream is None:
+                self.stream = torch.cuda.Stream(buf.device)
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(buf.device))
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ready)
+                self.dist.all_reduce(buf, op=self.dist.ReduceOp.SUM, group=self.group)
+                done = torch.cuda.Event()
+                done.record(self.stream)
+            return done
+        host = buf.cpu()
+        self.dist.all_reduce(host, op=self.dist.ReduceOp.SUM, group=self.group)
+        buf.copy_(host)
+        return None
+
+    def wait(self, handle, device) -> None:
+        if handle is not None:
+            torch.cuda.current_stream(device).wait_event(handle)
+
+
+def propagate_forward_reduced(x0u: torch.Tensor, x0i: torch.Tensor, rplan, K: int,
+                              reducer: ItemReducer) -> tuple[torch.Tensor, torch.Tensor]:
+    """(users [U, d], items [I, d]): the LightGCN final embedding of this row group's users (other
+    user rows unwritten) and of every item. x0u / x0i: the layer-0 tables (this rank's columns).
+
+    Layer k: the item partials from the users of layer k-1 (own rows), their all_reduce started;
+    then the users of layer k from the items of layer k-1 (reduced one layer earlier); then, once
+    layer k-1's reduction has landed, its item epilogue. Each reduction overlaps a user pass and
+    the next partial pass."""
+    U, d = x0u.shape
+    I = x0i.shape[0]
+    dev = x0u.device
+    div = float(K + 1)
+    mul = float(np.float32(1.0 / (K + 1)))
+    out_u = torch.empty((U, d), dtype=torch.float32, device=dev)
+    out_i = torch.empty((I, d), dtype=torch.float32, device=dev)
+    if K == 0:
+        return (x0u / div) * mul, (x0i / div) * mul
+    yu = [torch.empty((U, d), dtype=torch.float32, device=dev) for _ in range(min(2, K - 1))]
+    part = [torch.empty((I, d), dtype=torch.float32, device=dev) for _ in range(min(2, K))]
+    e = (x0u, x0i, U)
+    acc = (out_u, out_i, U)
+
+    def mode_of(k):
+        if K == 1:
+            return _ffi.EPI_FINAL_E
+        return _ffi.EPI_INIT if k == 1 else (_ffi.EPI_ADD if k < K else _ffi.EPI_FINAL_ACC)
+
+    pending = None  # (handle, layer) of the reduction in flight
+    for k in range(1, K + 1):
+        src_u = x0u if k == 1 else yu[(k - 2) % 2]
+        src_i = x0i if k == 1 else part[(k - 2) % 2]
+        mode = mode_of(k)
+        final = mode in (_ffi.EPI_FINAL_E, _ffi.EPI_FINAL_ACC)
+        pk = part[(k - 1) % 2]
+        rplan.run_partial(src_u, pk)
+        started = (reducer.start(pk), k)
+        if pending is not None:  # layer k-1's items: reduced before this layer's users read them
+            reducer.wait(pending[0], dev)
+            m = mode_of(pending[1])
+            rplan.run_item_epilogue(part[(pending[1] - 1) % 2], e, acc, m, 1.0, 1.0)
+        y = yu[(k - 1) % 2] if k < K else None
+        rplan.run_users(src_i, e if mode in (_ffi.EPI_INIT, _ffi.EPI_FINAL_E) else None, acc, y, mode,
+                        div if final else 1.0, mul if final else 1.0)
+        pending = started
+    reducer.wait(pending[0], dev)
+    rplan.run_item_epilogue(part[(K - 1) % 2], e, acc, mode_of(K), div, mul)
+    return out_u, out_i

@@ -34,6 +34,49 @@ import numpy as np
 from .propagate import propagate_backward_seeded, propagate_forward, spmm
 
 
+class ColumnGroup:
+    """This rank's share of column-sharded training (SURVEY §8e's parity-preserving alternative to
+    data parallelism): W ranks train the SAME batch with the same negatives, rank r holding columns
+    [r*d/W, (r+1)*d/W) of both tables and their Adam state. LightGCN never mixes columns, so the
+    propagation and the row-wise Adam need nothing from the other ranks; the cosine-BPR loss needs
+    each triplet's full-width dot products and norms (one all_reduce of [B, 6] per step) and
+    clip_grad_norm_ the full norm (one all_gather of the norm's block partials). The result is the
+    one-GPU step up to the association of those sums (reference utils/train_test.py:18-51,86-96)."""
+
+    def __init__(self, world: int, rank: int, d_full: int, group=None):
+        if d_full % world or (d_full // world) % 4:
+            raise ValueError(f"d={d_full} does not split into {world} column shares of a multiple of 4")
+        self.world, self.rank, self.d_full, self.group = int(world), int(rank), int(d_full), group
+        self.d = self.d_full // self.world
+
+    @property
+    def cols(self) -> tuple[int, int]:
+        return self.rank * self.d, (self.rank + 1) * self.d
+
+    def all_reduce(self, t: torch.Tensor) -> None:
+        import torch.distributed as dist
+
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
+    def gather_partials(self, part: torch.Tensor) -> torch.Tensor:
+        import torch.distributed as dist
+
+        if self.world == 1:
+            return part
+        out = torch.empty(self.world * part.numel(), dtype=part.dtype, device=part.device)
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(out, part, group=self.group)
+        else:
+            dist.all_gather(list(out.view(self.world, -1).unbind(0)), part, group=self.group)
+        return out
+
+    def reg_coeff(self, coeff: float) -> float:
+        """The coefficient whose kreg = c * 2 / (B * d) over this rank's d columns equals the full
+        width's coeff * 2 / (B * d_full) (the reg rows the scatters form, RegSrc)."""
+        return float(np.float32(float(coeff) * self.d / self.d_full))
+
+
 class _BatchState:
     def __init__(self, model, edge_index: torch.Tensor, d: int, lazy: bool = False):
         dev = edge_index.device
@@ -174,7 +217,8 @@ class FusedTrainStep:
     compute_grads(batch) -> loss: sets user/item_embedding.weight.grad only."""
 
     def __init__(self, model, optimizer, bpr_coeff: float = 5e-3, world: int = 1, max_entries: int = 4096,
-                 graphs: bool = False, lazy: bool = False, exchange=None, neg_seed: int | None = None):
+                 graphs: bool = False, lazy: bool = False, exchange=None, neg_seed: int | None = None,
+                 cols: ColumnGroup | None = None):
         """graphs=True: the first step of each batch runs eagerly, then the whole step (gradients
         and, at world == 1, the optimizer — which must be a capturable FusedAdam) is captured in a
         per-batch hipGraph and replayed from then on; negatives still come from the global CUDA
@@ -184,7 +228,9 @@ class FusedTrainStep:
         a lgcn_amd.owner.OwnerExchange (owner-sharded optimizer: step(batch, next_batch) — the
         rows of next_batch's step are fetched from their owners at the end of this one).
         neg_seed: draw step k's negatives from a generator seeded (neg_seed, k) instead of the
-        global CUDA generator (the same draws whichever exchange runs, and whenever they are drawn)."""
+        global CUDA generator (the same draws whichever exchange runs, and whenever they are drawn).
+        cols (lazy): column-sharded training — the model holds this rank's ColumnGroup columns,
+        every rank steps the same batches with the same negatives (the same neg_seed); eager."""
         self.model = model
         self.optimizer = optimizer
         self.coeff = float(bpr_coeff)
@@ -205,6 +251,12 @@ class FusedTrainStep:
         self._states: dict[int, tuple[weakref.ref, int, _BatchState]] = {}
         from .owner import OwnerExchange
 
+        self.cols = cols
+        if cols is not None:
+            if not lazy or exchange is not None or graphs:
+                raise ValueError("cols= needs lazy=True (RowLazyAdam), no exchange and graphs=False")
+            if model.dim_h != cols.d:
+                raise ValueError(f"the model holds {model.dim_h} columns, the ColumnGroup share is {cols.d}")
         self.owner = isinstance(exchange, OwnerExchange)
         if self.owner and not lazy:
             raise ValueError("an OwnerExchange needs lazy=True (RowLazyAdam)")
@@ -302,6 +354,33 @@ class FusedTrainStep:
         iw.grad = gi
         return st.loss
 
+    def _bpr(self, lib, st, out, uw, iw, U: int, N: int, B: int, d: int, div: float, mul: float, stream) -> float:
+        """The fused cosine-BPR kernel and the loss sum; returns the reg coefficient the scatters'
+        reg rows use. Column-sharded: this rank's partial sums, one all_reduce of [B, 6] over the
+        column groups, then the gradient rows of its columns from the full sums."""
+        c = self.cols
+        if c is None:
+            _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
+                                          st.users.data_ptr(), st.pos.data_ptr(), st.neg.data_ptr(), B, d,
+                                          st.plan.touched.data_ptr(), div, mul,
+                                          self.coeff, st.cf.data_ptr(), _ffi.ptr(st.cw), st.terms.data_ptr(),
+                                          stream), "lgcn_bpr_fused")
+            _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(),
+                                         st.loss_part.data_ptr(), stream), "lgcn_bpr_loss")
+            return self.coeff
+        if getattr(st, "sums", None) is None:
+            st.sums = torch.empty(max(1, 6 * B), dtype=torch.float32, device=uw.device)
+        args = (out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U, st.users.data_ptr(), st.pos.data_ptr(),
+                st.neg.data_ptr(), B, d, c.d_full, st.plan.touched.data_ptr(), div, mul, self.coeff,
+                st.sums.data_ptr())
+        _ffi.check(lib.lgcn_bpr_fused_cols(*args, 1, None, None, None, stream), "lgcn_bpr_fused_cols(partials)")
+        c.all_reduce(st.sums)
+        _ffi.check(lib.lgcn_bpr_fused_cols(*args, 2, st.cf.data_ptr(), _ffi.ptr(st.cw), st.terms.data_ptr(), stream),
+                   "lgcn_bpr_fused_cols")
+        _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, c.d_full, self.coeff, st.loss.data_ptr(),
+                                     st.loss_part.data_ptr(), stream), "lgcn_bpr_loss")
+        return c.reg_coeff(self.coeff)
+
     def _step_lazy(self, st: _BatchState, draw: bool = True) -> torch.Tensor:
         """The whole batch step with the row-lazy optimizer: catch the batch's rows (touched rows
         and this step's negatives) up, forward, loss, gradient rows written only where the step
@@ -331,23 +410,16 @@ class FusedTrainStep:
             if not self.owner:  # owner-sharded: the rows were fetched current by the previous step
                 opt.catch_up(st.touched_rows, st.neg, U)
             out = propagate_forward(uw.detach(), iw.detach(), st.plan, K)
-            _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
-                                          st.users.data_ptr(), st.pos.data_ptr(), st.neg.data_ptr(), B, d,
-                                          st.plan.touched.data_ptr(), div, mul,
-                                          self.coeff, st.cf.data_ptr(), _ffi.ptr(st.cw), st.terms.data_ptr(),
-                                          stream), "lgcn_bpr_fused")
-            _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(),
-                                         st.loss_part.data_ptr(), stream),
-                       "lgcn_bpr_loss")
+            reg_coeff = self._bpr(lib, st, out, uw, iw, U, N, B, d, div, mul, stream)
             gu, gi = opt.gu, opt.gi
             grads = (gu, gi, U)
             # seed g = (dF * mul) / div on every touched row (0 where no (user, positive) key)...
             spmm(st.fixed_touched, N, d, (st.cf, None, big), None, grads, None, _ffi.EPI_SCALE, div, mul,
                  stream=stream)
             # ... the negatives' rows added (stored where the row is outside the touched set)
-            scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream, uw, iw, self.coeff)
+            scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream, uw, iw, reg_coeff)
             propagate_backward_seeded(gu, gi, st.plan, K)
-            add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, self.coeff, stream)
+            add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, reg_coeff, stream)
             _ffi.check(lib.lgcn_flagged_rows_add(st.neg.data_ptr(), B, U, st.c2buf.data_ptr(),
                                                  st.c2flag.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U,
                                                  stream), "lgcn_flagged_rows_add")
@@ -378,7 +450,8 @@ class FusedTrainStep:
         with torch.no_grad():
             if ex is None:
                 opt.step_rows(st.touched_rows, st.neg, self.model.num_users, first_b=st.c2flag,
-                              skip_b=st.plan.touched)
+                              skip_b=st.plan.touched,
+                              gather_partials=self.cols.gather_partials if self.cols is not None else None)
                 return
             lib = _ffi.load()
             m = self.model

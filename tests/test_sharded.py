@@ -201,10 +201,133 @@ def test_grid_candidates():
 
     assert grid_candidates(1, 64) == [(1, 1, None)]
     assert grid_candidates(2, 64) == [(1, 2, None)]
-    rows_only = lambda w: [(w, 1, "allgather"), (w, 1, "p2p")]  # noqa: E731 (world >= 4: R - 1 >= 3 links)
-    assert grid_candidates(4, 64) == [(1, 4, None), (2, 2, "allgather")] + rows_only(4)
-    assert grid_candidates(8, 64) == [(1, 8, None), (2, 4, "allgather"), (4, 2, "allgather"), (4, 2, "p2p")] + rows_only(8)
+    # world >= 4: R - 1 >= 3 links; "reduce" (users sharded, items all-reduced) for every R > 1
+    rows_only = lambda w: [(w, 1, "allgather"), (w, 1, "p2p"), (w, 1, "reduce")]  # noqa: E731
+    assert grid_candidates(4, 64) == [(1, 4, None), (2, 2, "allgather"), (2, 2, "reduce")] + rows_only(4)
+    assert grid_candidates(8, 64) == [(1, 8, None), (2, 4, "allgather"), (2, 4, "reduce"), (4, 2, "allgather"),
+                                      (4, 2, "p2p"), (4, 2, "reduce")] + rows_only(8)
     assert grid_candidates(3, 64) == rows_only(3)   # odd world: rows only
-    assert grid_candidates(8, 32) == [(2, 4, "allgather"), (4, 2, "allgather"), (4, 2, "p2p")] + rows_only(8)  # 4-col shares: no
+    assert grid_candidates(8, 32) == [(2, 4, "allgather"), (2, 4, "reduce"), (4, 2, "allgather"), (4, 2, "p2p"),
+                                      (4, 2, "reduce")] + rows_only(8)  # 4-col shares: no
+    assert (4, 1, "reduce") not in grid_candidates(4, 64, bipartite=False)
     for R, F, _ in grid_candidates(8, 256):
         assert R * F == 8 and (256 // F) % 4 == 0
+
+
+class CpuReducePlan:
+    """Stand-in for ReducePlan on CPU: the three passes computed by the oracle restatement (the
+    whole graph's gcn_norm weights; the item partials over the edges this row group's users source,
+    summed in edge order), the epilogue applied to the rows each pass writes."""
+
+    def __init__(self, ei, shards, g):
+        from oracle import lgconv_ref as R
+
+        self.R, self.shards = R, shards
+        self.N, self.U = shards.N, shards.U
+        self.ei = ei
+        self.w = R.gcn_norm(ei, self.N)
+        ua, ub = shards.users(g)
+        self.own = np.arange(ua, ub)
+        sel = (ei[0] >= ua) & (ei[0] < ub)
+        self.ei_sub, self.w_sub = ei[:, sel], self.w[sel]
+        self.log = []
+
+    @staticmethod
+    def _epi(acc, e, rows, v, mode, div, mul):
+        if mode == _ffi.EPI_INIT:
+            acc[rows] = e[rows] + v
+        elif mode == _ffi.EPI_ADD:
+            acc[rows] = acc[rows] + v
+        elif mode == _ffi.EPI_FINAL_ACC:
+            acc[rows] = ((acc[rows] + v) / div) * mul
+        elif mode == _ffi.EPI_FINAL_E:
+            acc[rows] = ((e[rows] + v) / div) * mul
+        elif mode == _ffi.EPI_STORE:
+            acc[rows] = v
+
+    def run_partial(self, x_users, part_items):
+        self.log.append("partial")
+        x = np.zeros((self.N, x_users.shape[1]), np.float32)
+        x[:self.U] = x_users.numpy()
+        part_items[:] = torch.from_numpy(self.R.lgconv(x, self.ei_sub, self.w_sub)[self.U:])
+
+    def run_users(self, x_items, e, acc, y, mode, div, mul):
+        self.log.append("users")
+        x = np.zeros((self.N, x_items.shape[1]), np.float32)
+        x[self.U:] = x_items.numpy()
+        v = torch.from_numpy(self.R.lgconv(x, self.ei, self.w)[self.own])
+        self._epi(acc[0], e[0] if e is not None else None, self.own, v, mode, div, mul)
+        if y is not None and mode in (_ffi.EPI_INIT, _ffi.EPI_ADD):
+            y[self.own] = v
+
+    def run_item_epilogue(self, v_items, e, acc, mode, div, mul):
+        self.log.append("items")
+        rows = np.arange(self.N - self.U)
+        self._epi(acc[1], e[1], rows, v_items.clone(), mode, div, mul)
+
+
+def _reduce_worker(rank, world, port, kind, K, out_dir, F=1):
+    import sys
+
+    from conftest import PKG, ROOT
+    sys.path[:0] = [str(PKG), str(ROOT), str(ROOT / "tests")]
+    import graphs
+    from lgcn_amd.sharded import ItemReducer, ShardGrid, UserShards, propagate_forward_reduced
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    U, I, ei = _graph(kind)
+    grid = ShardGrid.build(world, rank, 16, world // F, F)
+    c0, c1 = grid.cols
+    g = grid.row_group
+    shards = UserShards.build(np.bincount(ei[1], minlength=U + I), U, grid.R)
+    plan = CpuReducePlan(ei, shards, g)
+    uw, iw = graphs.embeddings(U, I, 16, seed=K)
+    group = grid.exchange_group(dist)
+    red = ItemReducer(grid.R, group)
+    ou, oi = propagate_forward_reduced(torch.from_numpy(uw[:, c0:c1].copy()), torch.from_numpy(iw[:, c0:c1].copy()),
+                                       plan, K, red)
+    ua, ub = shards.users(g)
+    np.save(os.path.join(out_dir, f"u{g}_{grid.col_group}.npy"), ou[ua:ub].numpy())
+    np.save(os.path.join(out_dir, f"i{rank}.npy"), oi.numpy())
+    np.save(os.path.join(out_dir, f"log{rank}.npy"), np.array(plan.log))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,world,K,F", [("sym", 2, 3, 1), ("sub", 2, 3, 1), ("hub", 3, 4, 1), ("sym", 4, 2, 2),
+                                            ("sub", 4, 1, 1), ("hub", 2, 3, 1), ("sub", 8, 3, 2), ("sym", 2, 0, 1)])
+def test_reduce_mode_matches_oracle(tmp_path, kind, world, K, F):
+    """The reduce mode (users sharded, item rows all-reduced per layer) over gloo: every row group's
+    users and every rank's items within 1e-5 per row of the one-rank oracle forward (an item row is
+    the sum of R partial chains), the column groups' items identical across their row groups, and
+    the pass order of the overlapped schedule."""
+    import graphs
+    from oracle import lgconv_ref as R
+    from parity import assert_rows_close
+
+    from lgcn_amd.sharded import UserShards
+
+    U, I, ei = _graph(kind)
+    port = _free_port()
+    mp.spawn(_reduce_worker, args=(world, port, kind, K, str(tmp_path), F), nprocs=world, join=True)
+    uw, iw = graphs.embeddings(U, I, 16, seed=K)
+    ref = R.lightgcn_forward(uw, iw, ei, K)
+    ref = np.concatenate(ref) if isinstance(ref, tuple) else ref
+    shards = UserShards.build(np.bincount(ei[1], minlength=U + I), U, world // F)
+    w = 16 // F
+    for g in range(world // F):
+        ua, ub = shards.users(g)
+        got = np.concatenate([np.load(tmp_path / f"u{g}_{c}.npy") for c in range(F)], axis=1)
+        assert_rows_close(got, ref[ua:ub], what=f"users of row group {g}")
+    for r in range(world):
+        c = r % F
+        got = np.load(tmp_path / f"i{r}.npy")
+        assert_rows_close(got, ref[U:, c * w:(c + 1) * w], what=f"items on rank {r}")
+        same = np.load(tmp_path / f"i{c}.npy")
+        np.testing.assert_array_equal(got, same)
+    if K:
+        log = list(np.load(tmp_path / "log0.npy"))
+        expect = ["partial", "users"] + ["partial", "items", "users"] * (K - 1) + ["items"]
+        assert log == expect, log

@@ -4,4 +4,4 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=$1; shift
 O=gpurun_out/$TAG; mkdir -p $O
-timeout -k 10 900 python -u -m pytest "$@" -m gpu -x -v -s --timeout 600 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest "$@" -m gpu -v -s --timeout 600 --timeout-method thread > $O/pytest.log 2>&1
