@@ -356,6 +356,11 @@ def main():
     ap.add_argument("--no-graphs", action="store_true", help="train: run the fused step eagerly (no hipGraph replay)")
     ap.add_argument("--exchange", action="store_true",
                     help="train, N=1: run the row exchange anyway (measures its kernels; N>1 always uses it)")
+    ap.add_argument("--dp-mode", choices=["replicated", "owner", "columns"], default="replicated",
+                    help="train, N > 1: replicated row-lazy Adam (all_gather of every rank's gradient rows), "
+                         "owner-sharded Adam (rows to their owners, rows fetched for the next step: two "
+                         "all_to_alls), or column-sharded exact training (every rank the same batches on d/N "
+                         "columns: one [B, 6] all_reduce per step; the one-GPU step's semantics)")
     ap.add_argument("--dense-adam", action="store_true",
                     help="train: dense FusedAdam over all rows every step instead of the row-lazy exact Adam")
     ap.add_argument("--autograd", action="store_true",
@@ -728,6 +733,21 @@ def run_train(args):
     torch.manual_seed(0)
     model = LightGCN(U, I, num_layers=K, dim_h=d).to(dev)
     lazy = not (args.autograd or args.torch_adam or args.dense_adam)
+    dp_mode = args.dp_mode if world > 1 else "replicated"
+    if dp_mode != "replicated" and not lazy:
+        raise SystemExit("--dp-mode owner / columns need the row-lazy Adam (no --autograd/--torch-adam/--dense-adam)")
+    cols = None
+    if dp_mode == "columns":
+        from lgcn_amd.train_step import ColumnGroup
+
+        cols = ColumnGroup(world, rank, d)
+        c0, c1 = cols.cols
+        full = model
+        model = LightGCN(U, I, num_layers=K, dim_h=c1 - c0).to(dev)
+        with torch.no_grad():
+            model.user_embedding.weight.copy_(full.user_embedding.weight[:, c0:c1])
+            model.item_embedding.weight.copy_(full.item_embedding.weight[:, c0:c1])
+        del full
     if args.torch_adam:
         opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     elif lazy:
@@ -745,7 +765,15 @@ def run_train(args):
 
     fused = None
     exchange = None
-    if lazy and (world > 1 or args.exchange):
+    if dp_mode == "owner":
+        from lgcn_amd import _ffi
+        from lgcn_amd.owner import OwnerExchange, owner_capacity
+
+        exchange = OwnerExchange(owner_capacity(batches, U, world), N, d, dev, world, rank,
+                                 _ffi.load().lgcn_row_grad_norm_workspace_floats())
+        log(f"[rank {rank}] owner exchange: {exchange.cap} slots per destination, blocks of "
+            f"{exchange.blk * 4 / 1e6:.2f} MB, two all_to_alls per step")
+    elif dp_mode == "replicated" and lazy and (world > 1 or args.exchange):
         # row-sparse DP gradient exchange: all_gather of each rank's nonzero gradient rows
         cap = D.exchange_capacity(batches, U)
         exchange = D.RowExchange(cap, N, d, dev, world)
@@ -755,13 +783,18 @@ def run_train(args):
     if not args.autograd:
         from lgcn_amd.train_step import FusedTrainStep
 
-        fused = FusedTrainStep(model, opt, world=world, graphs=not args.no_graphs and not args.torch_adam,
-                               lazy=lazy, exchange=exchange)
+        fused = FusedTrainStep(model, opt, world=world if cols is None else 1,
+                               graphs=not args.no_graphs and not args.torch_adam and cols is None,
+                               lazy=lazy, exchange=exchange, cols=cols,
+                               neg_seed=(7 if cols is not None else 1000 + rank) if dp_mode != "replicated" else None)
 
-    def step(bidx):
+    def step(bidx, nxt=None):
         batch = batches[bidx]
         if fused is not None:
-            fused.step(batch)
+            if dp_mode == "owner":
+                fused.step(batch, batches[nxt] if nxt is not None else None)
+            else:
+                fused.step(batch)
             return batch.edge_index.shape[1]
         opt.zero_grad()
         loss = bpr_loss(*compute_embeddings(model, batch, dev))
@@ -772,18 +805,29 @@ def run_train(args):
         opt.step()
         return batch.edge_index.shape[1]
 
-    share = D.rank_share(len(batches), world, rank, seed=0, epoch=0)
-    for i in range(max(args.warmup, 2 * len(share))):  # warm-up builds every batch's plan
-        step(share[i % len(share)])
-        if fused is not None and (i + 1) % len(share) == 0:
+    # column-sharded ranks all step the one schedule (the one-GPU order); the DP modes split it
+    share = (D.rank_share(len(batches), 1, 0, seed=0, epoch=0) if cols is not None else
+             D.rank_share(len(batches), world, rank, seed=0, epoch=0))
+
+    def nxt_of(i, last):
+        """the batch index of step i + 1 (owner mode fetches its rows), None after an epoch's end
+        (sync() makes every row current there) or the run's last step"""
+        return None if (i + 1) % len(share) == 0 or i + 1 == last else share[(i + 1) % len(share)]
+
+    n_warm = max(args.warmup, 2 * len(share))
+    for i in range(n_warm):  # warm-up builds every batch's plan
+        step(share[i % len(share)], nxt_of(i, n_warm))
+        if fused is not None and ((i + 1) % len(share) == 0 or i + 1 == n_warm):
             fused.sync()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     edges = 0
+    if exchange is not None:
+        exchange.bytes = 0
     for i in range(args.steps):
-        edges += step(share[i % len(share)])
+        edges += step(share[i % len(share)], nxt_of(i, args.steps))
         # row-lazy Adam: parameters are made current once per epoch (as evaluation needs them),
         # inside the timed region
         if fused is not None and ((i + 1) % len(share) == 0 or i + 1 == args.steps):
@@ -799,12 +843,13 @@ def run_train(args):
         tt = t.clone()
         dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
-        elapsed, edges = float(t[0].item()), float(tt[1].item())
+        # column-sharded: every rank propagated the same batches (d / W columns each): count them once
+        elapsed, edges = float(t[0].item()), float(tt[1].item()) / (world if cols is not None else 1)
     result = {
         "metric": f"training edges propagated/sec (Cluster-GCN, K={K}, d={d})",
         "value": K * edges / elapsed, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "scaling": "strong" if cols is not None else "weak", "vs_baseline": None, "dtype": "fp32",
         "data": ("synthetic (seeded ML-25M-sized graph with 1024 planted communities, 90/5/5 directed split)"
                  if args.graph == "planted" else "synthetic (seeded ML-25M-shaped graph, 90/5/5 directed split)"),
         "config": {"workload": f"C{3 if world == 1 else 4}_cluster_gcn_train" + ("_planted" if args.graph == "planted" else ""),
@@ -816,11 +861,20 @@ def run_train(args):
                            ("fused sparse step" + ("" if (args.no_graphs or args.torch_adam) else ", hipGraph per batch")),
                    "parts_per_batch": q, "f_intra": f_intra, "layers": K, "dim": d, "num_users": U,
                    "num_items": I, "train_edges": n_tr,
-                   "parallelism": (f"dp{world}: disjoint part batches per rank, " +
-                                   ("row-sparse gradient exchange (one all_gather per step of each rank's nonzero rows and their ids), "
+                   "parallelism": (f"columns{world}: every rank the same batches and negatives on {d // world} of "
+                                   f"{d} columns; one all_reduce of the triplets' [B, 6] dots/norms and one "
+                                   f"all_gather of the clip norm's partials per step (the one-GPU step's semantics)"
+                                   if cols is not None else
+                                   f"dp{world}: disjoint part batches per rank, " +
+                                   ("owner-sharded row-lazy Adam (row r owned by rank r % W): gradient rows to their "
+                                    "owners and the next step's rows back, two all_to_alls + the clip norm's "
+                                    "partials per step" if dp_mode == "owner" else
+                                    "row-sparse gradient exchange (one all_gather per step of each rank's nonzero rows and their ids), "
                                     "row-lazy Adam on the union" if exchange is not None else
                                     "RCCL all_reduce of embedding grads" if world > 1 else "single GPU"))},
     }
+    if exchange is not None and hasattr(exchange, "bytes"):
+        result["exchange"] = {"mode": dp_mode, "MB_received_per_rank_per_step": exchange.bytes / args.steps / 1e6}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -112,7 +112,9 @@ int lgcn_csr_build(const int64_t* key, const int64_t* other, int64_t E, int64_t 
  * B, R, ...) writes rowptr and eid (positions b grouped by key[b], ascending b inside a key; an
  * out-of-range key counts in *err_count and is grouped under key 0, as there). A counting sort:
  * one atomic count per key, one scan, atomic placement, then each key's few positions put in
- * ascending order. cursor: device int32[R] scratch. Meant for many keys over a small range with
+ * ascending order. cursor: device int32[R] scratch, all zero on entry (allocate it zeroed) and
+ * left all zero on exit — no memset, so the call captures into a hipGraph as kernels only.
+ * Meant for many keys over a small range with
  * short groups (the per-step negatives, B ~ 1.8e5 over I = 59,047 items: ~3 per key); a group's
  * ordering is quadratic in its length. B < 2^31, R < 2^31.
  * Replaces: the per-step grouping that index_put_(accumulate) performs implicitly in the

@@ -471,10 +471,13 @@ __global__ void k_group_place(const int64_t* __restrict__ key, int64_t B, int64_
     }
 }
 
-// Each key's positions in ascending order (insertion sort; groups are a few entries long).
-__global__ void k_group_order(const int64_t* __restrict__ rowptr, int64_t R, int32_t* __restrict__ perm) {
+// Each key's positions in ascending order (insertion sort; groups are a few entries long); the
+// cursor is zeroed for the next call (no memset node in a captured step).
+__global__ void k_group_order(const int64_t* __restrict__ rowptr, int64_t R, int32_t* __restrict__ perm,
+                              int32_t* __restrict__ cursor) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < R; r += stride) {
+        cursor[r] = 0;
         const int64_t beg = rowptr[r], end = rowptr[r + 1];
         for (int64_t i = beg + 1; i < end; ++i) {
             const int32_t v = perm[i];
@@ -552,7 +555,6 @@ int lgcn_group_keys(const int64_t* key, int64_t B, int64_t R, int64_t* rowptr, i
     if (B > INT32_MAX || R > INT32_MAX)
         return fail(LGCN_E_UNSUPPORTED, "lgcn_group_keys: B=%lld R=%lld exceed int32", (long long)B, (long long)R);
     hipStream_t s = as_stream(stream);
-    if (int rc = check_hip(hipMemsetAsync(cursor, 0, sizeof(int32_t) * R, s), "memset cursor")) return rc;
     auto* err = reinterpret_cast<unsigned long long*>(err_count);
     if (B > 0) {
         k_group_count<<<grid_for(B, kBlock, 4096), kBlock, 0, s>>>(key, B, R, cursor, err);
@@ -560,10 +562,11 @@ int lgcn_group_keys(const int64_t* key, int64_t B, int64_t R, int64_t* rowptr, i
     }
     k_group_scan<<<1, kScanBlock, 0, s>>>(cursor, R, rowptr);
     if (int rc = check_launch("k_group_scan")) return rc;
-    if (B == 0) return LGCN_OK;
-    k_group_place<<<grid_for(B, kBlock, 4096), kBlock, 0, s>>>(key, B, R, rowptr, cursor, perm, err);
-    if (int rc = check_launch("k_group_place")) return rc;
-    k_group_order<<<grid_for(R, kBlock, 4096), kBlock, 0, s>>>(rowptr, R, perm);
+    if (B > 0) {
+        k_group_place<<<grid_for(B, kBlock, 4096), kBlock, 0, s>>>(key, B, R, rowptr, cursor, perm, err);
+        if (int rc = check_launch("k_group_place")) return rc;
+    }
+    k_group_order<<<grid_for(R, kBlock, 4096), kBlock, 0, s>>>(rowptr, R, perm, cursor);
     return check_launch("k_group_order");
 }
 

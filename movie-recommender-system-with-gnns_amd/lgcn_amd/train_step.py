@@ -127,7 +127,8 @@ class _BatchState:
                 _ffi.check(lib_.lgcn_csr_workspace_size(B, I, nb), "lgcn_csr_workspace_size")
                 self.neg_ws = torch.empty(max(1, nb.value), dtype=torch.uint8, device=dev)
             else:
-                self.neg_cursor = torch.empty(max(1, I), dtype=torch.int32, device=dev)
+                # all zero between calls (lgcn_group_keys leaves it zeroed)
+                self.neg_cursor = torch.zeros(max(1, I), dtype=torch.int32, device=dev)
         else:
             self.neg_rowptr = None
         if self.small:
@@ -264,6 +265,7 @@ class FusedTrainStep:
         self._gen = None
         self._k = 0  # steps taken (the index of the next step)
         self._owner_graphs = None
+        self._synced = True  # every row current on every rank (start, or after sync())
 
     def state(self, edge_index: torch.Tensor) -> _BatchState:
         hit = self._states.get(id(edge_index))

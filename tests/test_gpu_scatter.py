@@ -251,9 +251,12 @@ def _group_both(gpu, keys_np, R):
         perm = torch.full((max(B, 1),), -7, dtype=torch.int32, device=gpu)
         err = torch.zeros(1, dtype=torch.int64, device=gpu)
         if how == "group":
-            cursor = torch.full((R,), 123, dtype=torch.int32, device=gpu)  # garbage: the call zeroes it
-            _ffi.check(lib.lgcn_group_keys(keys.data_ptr(), B, R, rowptr.data_ptr(), perm.data_ptr(),
-                                           cursor.data_ptr(), err.data_ptr(), s), "lgcn_group_keys")
+            cursor = torch.zeros(R, dtype=torch.int32, device=gpu)  # zero on entry, zero again on exit
+            for _ in range(2):  # twice: the second call runs on the cursor the first one left
+                err.zero_()
+                _ffi.check(lib.lgcn_group_keys(keys.data_ptr(), B, R, rowptr.data_ptr(), perm.data_ptr(),
+                                               cursor.data_ptr(), err.data_ptr(), s), "lgcn_group_keys")
+            assert int(cursor.abs().sum().item()) == 0
         else:
             col = torch.empty(max(B, 1), dtype=torch.int32, device=gpu)
             nb = _ffi._sz(0)

@@ -1,5 +1,7 @@
 #!/bin/bash
 # Run a subset of the -m gpu tests (args: pytest selectors) on the box, log under gpurun_out/TAG.
+# Exit status: pytest's, so a caller can go on after plain test failures (1) but must stop after
+# a crash, abort or time limit (>= 2: 124/134/137/139 ...).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=$1; shift
