@@ -112,8 +112,9 @@ int lgcn_csr_build(const int64_t* key, const int64_t* other, int64_t E, int64_t 
  * B, R, ...) writes rowptr and eid (positions b grouped by key[b], ascending b inside a key; an
  * out-of-range key counts in *err_count and is grouped under key 0, as there). A counting sort:
  * one atomic count per key, one scan, atomic placement, then each key's few positions put in
- * ascending order. cursor: device int32[R] scratch, all zero on entry (allocate it zeroed) and
- * left all zero on exit — no memset, so the call captures into a hipGraph as kernels only.
+ * ascending order. cursor: device int32[lgcn_group_keys_cursor_len(R)] scratch whose first R
+ * entries are zero on entry (allocate it zeroed) and are left zero on exit — no memset, so the
+ * call captures into a hipGraph as kernels only (the tail holds per-tile totals).
  * Meant for many keys over a small range with
  * short groups (the per-step negatives, B ~ 1.8e5 over I = 59,047 items: ~3 per key); a group's
  * ordering is quadratic in its length. B < 2^31, R < 2^31.
@@ -122,6 +123,7 @@ int lgcn_csr_build(const int64_t* key, const int64_t* other, int64_t E, int64_t 
  * negatives from utils/helpers.py:64-82). */
 int lgcn_group_keys(const int64_t* key, int64_t B, int64_t R, int64_t* rowptr, int32_t* perm, int32_t* cursor,
                     int64_t* err_count, lgcn_stream_t stream);
+int64_t lgcn_group_keys_cursor_len(int64_t R);
 
 /* gcn_norm(add_self_loops=False), PyG 2.4.0: deg = in-degree (count of edges whose target
  * is the node), dis = deg^-1/2 with inf -> 0 (computed as 1/sqrt(deg), correctly rounded
@@ -349,6 +351,14 @@ int lgcn_sorted_scatter_add(const int64_t* rowptr, const int32_t* perm, int64_t 
  * kreg * W[r] added in sequence (kreg as in lgcn_range_scatter_add). rows (device int32[n_rows],
  * nullable): the rows to visit (NULL: rows 0 .. n_rows-1). Replaces a [2B, d] reg table and its
  * ADD pass (reference utils/train_test.py:38-41, the reg term's gradient). */
+/* The grouped negatives' reg-gradient rows after the backward: for every key r in [0, nrows) with
+ * n = rowptr[r+1] - rowptr[r] > 0, out[r + key_offset] += n copies of coeff * 2 / (B * d) *
+ * W[r + key_offset] added in sequence — what the sorted scatter would park per row and
+ * lgcn_flagged_rows_add add back, without the [B, d] parking table. (lgcn_sorted_scatter_add writes
+ * the first-occurrence flags whenever c2flag is given, parking or not.) */
+int lgcn_grouped_reg_add(const int64_t* rowptr, int64_t nrows, int64_t key_offset, const float* w_lo,
+                         const float* w_hi, int64_t w_split, int32_t d, float coeff, int64_t B, float* out_lo,
+                         float* out_hi, int64_t split, lgcn_stream_t stream);
 int lgcn_reg_rows_add(const int64_t* rowptr, const int32_t* rows, int64_t n_rows, const float* w_lo, const float* w_hi,
                       int64_t w_split, int32_t d, float coeff, int64_t B, float* out_lo, float* out_hi, int64_t split,
                       lgcn_stream_t stream);

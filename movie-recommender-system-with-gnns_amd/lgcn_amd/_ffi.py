@@ -41,6 +41,7 @@ _SIGS = {
     "lgcn_csr_workspace_size": ([_i64, _i64, ctypes.POINTER(_sz)], ctypes.c_int),
     "lgcn_csr_build": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
     "lgcn_group_keys": ([_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
+    "lgcn_group_keys_cursor_len": ([_i64], _i64),
     "lgcn_inv_sqrt_degree": ([_vp, _i64, _vp, _vp], ctypes.c_int),
     "lgcn_edge_norm": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_schedule_workspace_size": ([_i64, _i64, _i32, ctypes.POINTER(_sz)], ctypes.c_int),
@@ -76,6 +77,7 @@ _SIGS = {
                                 _f32, _i64, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_sorted_scatter_add": ([_vp, _vp, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _i64,
                                  _f32, _i64, _vp, _vp, _vp, _vp], ctypes.c_int),
+    "lgcn_grouped_reg_add": ([_vp, _i64, _i64, _vp, _vp, _i64, _i32, _f32, _i64, _vp, _vp, _i64, _vp], ctypes.c_int),
     "lgcn_reg_rows_add": ([_vp, _vp, _i64, _vp, _vp, _i64, _i32, _f32, _i64, _vp, _vp, _i64, _vp], ctypes.c_int),
     "lgcn_adam_consts": ([_vp, _i64, _i64, _f32, ctypes.c_double, ctypes.c_double, _vp], ctypes.c_int),
     "lgcn_row_adam": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64,

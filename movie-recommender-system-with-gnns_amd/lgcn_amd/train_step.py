@@ -128,14 +128,17 @@ class _BatchState:
                 self.neg_ws = torch.empty(max(1, nb.value), dtype=torch.uint8, device=dev)
             else:
                 # all zero between calls (lgcn_group_keys leaves it zeroed)
-                self.neg_cursor = torch.zeros(max(1, I), dtype=torch.int32, device=dev)
+                n_cur = int(_ffi.load().lgcn_group_keys_cursor_len(max(1, I)))
+                self.neg_cursor = torch.zeros(n_cur, dtype=torch.int32, device=dev)
         else:
             self.neg_rowptr = None
         if self.small:
             # the rows holding (user, positive) keys: lgcn_reg_rows_add visits only these
             rp = self.fixed_sparse.rowptr
             self.reg_rows = torch.nonzero(rp[1:] > rp[:-1]).squeeze(1).to(torch.int32).contiguous()
-            self.c2buf = torch.empty((B, d), dtype=torch.float32, device=dev)
+            # the range scatter parks each negative row's reg sum here; the sorted path forms them
+            # after the backward instead (add_negative_reg_rows), so it needs no [B, d] table
+            self.c2buf = torch.empty((B if self.neg_rowptr is None else 1, d), dtype=torch.float32, device=dev)
             self.c2flag = torch.empty(B, dtype=torch.uint8, device=dev)
             self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         self.cf = torch.empty((3 * B, d), dtype=torch.float32, device=dev)
@@ -178,9 +181,9 @@ def sorted_scatter_min_b() -> int:
 
 def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: float, store_unless, stream,
                       uw, iw, coeff: float) -> None:
-    """dF rows of the step's negatives into the gradient tables, their reg rows' sums (formed from
-    the layer-0 rows uw / iw) parked per row (first-occurrence slot, st.c2flag) for
-    lgcn_flagged_rows_add after the backward."""
+    """dF rows of the step's negatives into the gradient tables and the first-occurrence flags
+    (st.c2flag); the range scatter also parks each row's reg-rows sum (formed from the layer-0
+    rows uw / iw) in its first-occurrence slot for add_negative_reg_rows after the backward."""
     B = st.B
     C = st.cf[2 * B:]
     reg = (None, uw.data_ptr(), iw.data_ptr(), U, coeff, B)
@@ -198,10 +201,25 @@ def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: 
         _ffi.check(lib.lgcn_group_keys(st.neg.data_ptr(), B, I, st.neg_rowptr.data_ptr(), st.neg_perm.data_ptr(),
                                        st.neg_cursor.data_ptr(), st.neg_err.data_ptr(), stream),
                    "lgcn_group_keys(negatives)")
+    # sorted path: no parked reg sums (add_negative_reg_rows forms them per row after the backward);
+    # the first-occurrence flags are still written
     _ffi.check(lib.lgcn_sorted_scatter_add(st.neg_rowptr.data_ptr(), st.neg_perm.data_ptr(), I, U, C.data_ptr(), d,
-                                           gu.data_ptr(), gi.data_ptr(), U, mul, div, *reg,
+                                           gu.data_ptr(), gi.data_ptr(), U, mul, div, None, None, None, 0, 0.0, 0,
                                            st.c2buf.data_ptr(), st.c2flag.data_ptr(), _ffi.ptr(store_unless), stream),
                "lgcn_sorted_scatter_add")
+
+
+def add_negative_reg_rows(lib, st, gu, gi, U: int, d: int, uw, iw, coeff: float, stream) -> None:
+    """The negatives' reg-gradient rows, after the backward: the range scatter's parked per-row sums
+    (lgcn_flagged_rows_add), or — sorted path — the same n-copies sums formed per grouped row
+    (lgcn_grouped_reg_add: no [B, d] parking table written and read back)."""
+    if st.neg_rowptr is None:
+        _ffi.check(lib.lgcn_flagged_rows_add(st.neg.data_ptr(), st.B, U, st.c2buf.data_ptr(), st.c2flag.data_ptr(), d,
+                                             gu.data_ptr(), gi.data_ptr(), U, stream), "lgcn_flagged_rows_add")
+        return
+    _ffi.check(lib.lgcn_grouped_reg_add(st.neg_rowptr.data_ptr(), st.neg_rowptr.numel() - 1, U, uw.data_ptr(),
+                                        iw.data_ptr(), U, d, coeff, st.B, gu.data_ptr(), gi.data_ptr(), U, stream),
+               "lgcn_grouped_reg_add")
 
 
 def add_fixed_reg_rows(lib, st, gu, gi, U: int, N: int, d: int, uw, iw, coeff: float, stream) -> None:
@@ -337,9 +355,7 @@ class FusedTrainStep:
                 scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, None, stream, uw, iw, self.coeff)
                 propagate_backward_seeded(gu, gi, st.plan, K)
                 add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, self.coeff, stream)
-                _ffi.check(lib.lgcn_flagged_rows_add(st.neg.data_ptr(), B, U, st.c2buf.data_ptr(),
-                                                     st.c2flag.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U,
-                                                     stream), "lgcn_flagged_rows_add")
+                add_negative_reg_rows(lib, st, gu, gi, U, d, uw, iw, self.coeff, stream)
             else:
                 # large batches: one stable radix sort of all 3B row keys per step
                 _ffi.check(lib.lgcn_csr_build(st.keys.data_ptr(), st.keys.data_ptr(), 3 * B, N, st.rowptr.data_ptr(),
@@ -422,9 +438,7 @@ class FusedTrainStep:
             scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream, uw, iw, reg_coeff)
             propagate_backward_seeded(gu, gi, st.plan, K)
             add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, reg_coeff, stream)
-            _ffi.check(lib.lgcn_flagged_rows_add(st.neg.data_ptr(), B, U, st.c2buf.data_ptr(),
-                                                 st.c2flag.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U,
-                                                 stream), "lgcn_flagged_rows_add")
+            add_negative_reg_rows(lib, st, gu, gi, U, d, uw, iw, reg_coeff, stream)
             ex = self.exchange
             if self.owner:
                 # this rank's rows with a possibly nonzero gradient -> their owners' blocks

@@ -251,12 +251,12 @@ def _group_both(gpu, keys_np, R):
         perm = torch.full((max(B, 1),), -7, dtype=torch.int32, device=gpu)
         err = torch.zeros(1, dtype=torch.int64, device=gpu)
         if how == "group":
-            cursor = torch.zeros(R, dtype=torch.int32, device=gpu)  # zero on entry, zero again on exit
+            cursor = torch.zeros(int(lib.lgcn_group_keys_cursor_len(R)), dtype=torch.int32, device=gpu)
             for _ in range(2):  # twice: the second call runs on the cursor the first one left
                 err.zero_()
                 _ffi.check(lib.lgcn_group_keys(keys.data_ptr(), B, R, rowptr.data_ptr(), perm.data_ptr(),
                                                cursor.data_ptr(), err.data_ptr(), s), "lgcn_group_keys")
-            assert int(cursor.abs().sum().item()) == 0
+            assert int(cursor[:R].abs().sum().item()) == 0  # zero on entry, zero again on exit
         else:
             col = torch.empty(max(B, 1), dtype=torch.int32, device=gpu)
             nb = _ffi._sz(0)
@@ -299,3 +299,51 @@ def test_group_keys_out_of_range_keys(gpu):
     assert e_g == e_c == 3
     np.testing.assert_array_equal(rp_g, rp_c)
     np.testing.assert_array_equal(pm_g, pm_c)
+
+
+@pytest.mark.parametrize("B,nrows,d", [(3000, 500, 64), (20000, 59047, 128), (5000, 40, 32), (180000, 59047, 128)])
+def test_sorted_no_parking_plus_grouped_reg_equals_parked(gpu, B, nrows, d):
+    """The sorted path without the parking table (lgcn_sorted_scatter_add with no second source:
+    dF rows + flags, its C rows loaded four at a time) followed by lgcn_grouped_reg_add is bitwise
+    the parked path (reg sums parked per row, then lgcn_flagged_rows_add): the same n-copies sums
+    added to the same rows; the flags are the same."""
+    from lgcn_amd import _ffi
+
+    lib = _ffi.load()
+    rng = np.random.default_rng(B + 3 * d)
+    keys_np = rng.integers(0, nrows, B)
+    off = 9
+    N = off + nrows + 1
+    W = (rng.standard_normal((N, d)) * 0.1).astype(np.float32)
+    coeff = 5e-3
+    s = _ffi.stream_of(gpu)
+    keys = torch.from_numpy(keys_np.astype(np.int64)).to(gpu)
+    C = torch.from_numpy(rng.standard_normal((B, d)).astype(np.float32)).to(gpu)
+    Wg = torch.from_numpy(W).to(gpu)
+    split = off + nrows // 2
+    rowptr = torch.empty(nrows + 1, dtype=torch.int64, device=gpu)
+    perm = torch.empty(B, dtype=torch.int32, device=gpu)
+    cursor = torch.zeros(int(lib.lgcn_group_keys_cursor_len(nrows)), dtype=torch.int32, device=gpu)
+    err = torch.zeros(1, dtype=torch.int64, device=gpu)
+    _ffi.check(lib.lgcn_group_keys(keys.data_ptr(), B, nrows, rowptr.data_ptr(), perm.data_ptr(), cursor.data_ptr(),
+                                   err.data_ptr(), s), "group")
+    res = []
+    for park in (True, False):
+        out = torch.from_numpy(W * 0.5).to(gpu)
+        buf = torch.zeros((B, d), device=gpu)
+        flag = torch.full((B,), 7, dtype=torch.uint8, device=gpu)
+        reg = (None, Wg[:split].data_ptr(), Wg[split:].data_ptr(), split, coeff, B) if park else \
+              (None, None, None, 0, 0.0, 0)
+        _ffi.check(lib.lgcn_sorted_scatter_add(rowptr.data_ptr(), perm.data_ptr(), nrows, off, C.data_ptr(), d,
+                                               out[:split].data_ptr(), out[split:].data_ptr(), split, 0.25, 4.0,
+                                               *reg, buf.data_ptr(), flag.data_ptr(), None, s), "sorted")
+        if park:
+            _ffi.check(lib.lgcn_flagged_rows_add(keys.data_ptr(), B, off, buf.data_ptr(), flag.data_ptr(), d,
+                                                 out[:split].data_ptr(), out[split:].data_ptr(), split, s), "flagged")
+        else:
+            _ffi.check(lib.lgcn_grouped_reg_add(rowptr.data_ptr(), nrows, off, Wg[:split].data_ptr(),
+                                                Wg[split:].data_ptr(), split, d, coeff, B, out[:split].data_ptr(),
+                                                out[split:].data_ptr(), split, s), "grouped reg")
+        res.append((out.cpu(), flag.cpu()))
+    assert torch.equal(res[0][1], res[1][1])
+    assert torch.equal(res[0][0], res[1][0])

@@ -1,0 +1,78 @@
+"""Probe: one rank's compute share of the reduce-mode sharded C2 forward (lgcn_amd.sharded.
+ReducePlan: users sharded, item partials all-reduced) on one GPU, per R x F grid, without the
+all_reduce (a stand-in reducer that moves nothing): the time a rank spends in its kernels per K=3
+step, next to the bytes a ring all_reduce of its item partials moves per rank.
+python tools/reduce_rank_probe.py [--grids 2x1,4x1,8x1,2x2,4x2,2x4]"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "movie-recommender-system-with-gnns_amd"))
+
+from lgcn_amd import synth  # noqa: E402
+from lgcn_amd.sharded import ReducePlan, ShardGrid, UserShards, propagate_forward_reduced  # noqa: E402
+
+
+class NoReduce:
+    """The reducer's interface, moving nothing (the compute side alone)."""
+
+    def __init__(self, R):
+        self.R, self.bytes = R, 0
+
+    def start(self, buf):
+        self.bytes += int(2 * (self.R - 1) / self.R * buf.numel() * buf.element_size())
+        return None
+
+    def wait(self, handle, device):
+        pass
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--grids", default="2x1,4x1,8x1,2x2,4x2,2x4")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--chunk", type=int, default=256)
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    g = synth.ml25m_shaped(seed=0)
+    U, I, N = g.num_users, g.num_items, g.num_nodes
+    ei = torch.from_numpy(g.edge_index).to(dev)
+    deg = np.bincount(g.edge_index[1], minlength=N)
+    K, d = 3, 64
+    gen = torch.Generator(device=dev).manual_seed(0)
+    uw = torch.randn(U, d, device=dev, generator=gen) * 0.01
+    iw = torch.randn(I, d, device=dev, generator=gen) * 0.01
+    for spec in args.grids.split(","):
+        R, F = (int(v) for v in spec.split("x"))
+        grid = ShardGrid.build(R * F, 0, d, R, F)
+        c0, c1 = grid.cols
+        shards = UserShards.build(deg, U, R)
+        times, moved = [], 0
+        for gr in sorted({0, R - 1}):
+            rplan = ReducePlan(ei, shards, gr, c1 - c0, args.chunk)
+            x0u, x0i = uw[:, c0:c1].contiguous(), iw[:, c0:c1].contiguous()
+            red = NoReduce(R)
+            with torch.no_grad():
+                for _ in range(3):
+                    propagate_forward_reduced(x0u, x0i, rplan, K, red)
+                torch.cuda.synchronize()
+                red.bytes = 0
+                t = time.perf_counter()
+                for _ in range(args.steps):
+                    propagate_forward_reduced(x0u, x0i, rplan, K, red)
+                torch.cuda.synchronize()
+            times.append((time.perf_counter() - t) / args.steps * 1e3)
+            moved = red.bytes / args.steps
+            del rplan
+        print(f"grid {R}x{F} reduce: rank compute {max(times):.3f} ms/step (row groups {sorted({0, R - 1})}: "
+              f"{', '.join(f'{t:.3f}' for t in times)}); ring all_reduce bytes per rank per step {moved / 1e6:.1f} MB",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
