@@ -31,7 +31,7 @@ DEFAULT_CHUNK = 256
 SLICED_CHUNK = 192
 # hub chunk of the plain schedule the sharded forward's ranks run when R > 1 (lgcn_amd.sharded.
 # rank_chunk): per-rank K=3 step at 8 x 1 0.246 ms at 128, 0.253 at 256 (profiles/r02k_shard/)
-RANK_CHUNK = 128
+RANK_CHUNK = int(os.environ.get("LGCN_RANK_CHUNK", 128))  # (env: A/B knob)
 
 
 def sliced_chunk(chunk: int) -> int:
