@@ -75,3 +75,29 @@ def test_bench_main_becomes_the_launcher(tmp_path):
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode != 0
     assert "launch: 2 rank processes" in r.stderr
+
+
+def test_traffic_entry_needs_a_matching_signature(tmp_path, monkeypatch):
+    """roofline.traffic comes from profiles/pmc_traffic.json only when the entry's recorded plan
+    signature equals the run's; any difference (kernel source, launches, graph) falls back."""
+    b = _bench()
+    sig = b.traffic_signature("W", "k<16>", 7, 100, 1000, {"user_max": 5})
+    assert sig["kernel_source_sha16"] == b.kernel_source_sha16() and len(sig["kernel_source_sha16"]) == 16
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(b, "ROOT", tmp_path)
+    assert b.load_traffic(sig)[0] is None  # no file
+    (prof / "pmc_traffic.json").write_text(json.dumps({"W": {"hbm_bytes_per_launch": 123.0, "signature": sig}}))
+    assert b.load_traffic(sig) == (123.0, None)
+    other = dict(sig, launches_per_layer=8)
+    val, why = b.load_traffic(other)
+    assert val is None and "launches_per_layer" in why
+    (prof / "pmc_traffic.json").write_text(json.dumps({"W": {"hbm_bytes_per_launch": 123.0}}))  # no signature
+    assert b.load_traffic(sig)[0] is None
+
+
+def test_committed_c2_entry_matches_its_kernel_source():
+    """The committed C2 PMC entry was measured on the kernel source in the tree."""
+    b = _bench()
+    ent = json.loads((ROOT / "profiles" / "pmc_traffic.json").read_text())["C2_ml25m_shaped_K3_d64"]
+    assert ent["signature"]["kernel_source_sha16"] == b.kernel_source_sha16()
