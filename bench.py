@@ -177,9 +177,37 @@ def launch_ranks(n: int, argv: list, script=None) -> int:
     port = free_port()
     cmd = [sys.executable, "-u", str(script or pathlib.Path(__file__).resolve()), *argv]
     log(f"launch: {n} rank processes on 127.0.0.1:{port}: {' '.join(cmd[2:])}")
+
+    def die_with_parent():
+        # a rank gets SIGTERM if this launcher dies (even by SIGKILL): no orphan holds a GPU
+        import ctypes
+
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))  # PR_SET_PDEATHSIG
+
     procs = [subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if i == 0 else subprocess.DEVNULL,
-                              start_new_session=True)
+                              start_new_session=True, preexec_fn=die_with_parent)
              for i, e in enumerate(child_envs(n, port))]
+
+    def stop_all(signum, frame):
+        # the launcher was told to stop (a driver timeout): stop every rank's process group, then go
+        for q in procs:
+            try:
+                os.killpg(q.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        deadline = time.monotonic() + 20
+        for q in procs:
+            try:
+                q.wait(timeout=max(0.1, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(q.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+        sys.exit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, stop_all)
     import threading
 
     out = []

@@ -8,6 +8,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 from conftest import ROOT
 
 
@@ -101,3 +103,32 @@ def test_committed_c2_entry_matches_its_kernel_source():
     b = _bench()
     ent = json.loads((ROOT / "profiles" / "pmc_traffic.json").read_text())["C2_ml25m_shaped_K3_d64"]
     assert ent["signature"]["kernel_source_sha16"] == b.kernel_source_sha16()
+
+
+def test_launcher_stops_its_ranks_when_stopped(tmp_path):
+    """SIGTERM to the launcher (a driver timeout) stops every rank; none is left running."""
+    import signal
+    import time
+
+    prog = tmp_path / "sleeper.py"
+    pids = tmp_path / "pids"
+    pids.mkdir()
+    prog.write_text("import os, time, pathlib\n"
+                    f"pathlib.Path({str(pids)!r}, str(os.getpid())).write_text('x')\n"
+                    "time.sleep(600)\n")
+    launcher = tmp_path / "launch.py"
+    launcher.write_text("import importlib.util, sys\n"
+                        f"spec = importlib.util.spec_from_file_location('b', {str(ROOT / 'bench.py')!r})\n"
+                        "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
+                        f"sys.exit(b.launch_ranks(3, [], script={str(prog)!r}))\n")
+    p = subprocess.Popen([sys.executable, str(launcher)])
+    deadline = time.time() + 60
+    while len(list(pids.iterdir())) < 3 and time.time() < deadline:
+        time.sleep(0.2)
+    assert len(list(pids.iterdir())) == 3
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=60) == 128 + signal.SIGTERM
+    time.sleep(0.5)
+    for f in pids.iterdir():
+        with pytest.raises(ProcessLookupError):
+            os.kill(int(f.name), 0)
