@@ -556,6 +556,8 @@ class FusedTrainStep:
         if opt.max_grad_norm is not None:
             ex.gather_partials()
         if graphs_ok:
+            if opt.steps + 1 > opt.max_steps:
+                raise RuntimeError(f"RowLazyAdam: more than max_steps={opt.max_steps} steps")
             self._owner_graphs[1].replay()
             opt.steps += 1
         else:
@@ -593,8 +595,11 @@ class FusedTrainStep:
             self.optimizer.flush()
 
     def check_overflow(self) -> None:
-        """Raise if any step's negative scatter overflowed a workgroup list (never expected for
-        uniform negatives; one host read per batch state — call once per epoch)."""
+        """Raise if any step's negative scatter overflowed a workgroup list, or (owner-sharded) a
+        destination block (never expected for uniform negatives; one host read per batch state —
+        call once per epoch)."""
+        if self.owner:
+            self.exchange.check_overflow()
         for ref, _, st in self._states.values():
             if getattr(st, "overflow", None) is not None and int(st.overflow.item()):
                 raise RuntimeError("lgcn_range_scatter_add overflowed: negatives too concentrated for its lists")
