@@ -517,8 +517,9 @@ class UserShards:
         return int(self.ub[g]), int(self.ub[g + 1])
 
 
-def _identity_items(U: int, N: int, dev, chunk: int, stream) -> object:
-    """The plain schedule of weight-1 self edges on the item rows (the item epilogue pass)."""
+def _identity_items(U: int, N: int, dev, chunk: int, stream, rows: tuple[int, int] | None = None) -> object:
+    """The plain schedule of weight-1 self edges on the item rows (the item epilogue pass), or on
+    the item rows [U + a, U + b) only."""
     from .plan import CsrDirection, _schedule
 
     I = N - U
@@ -527,7 +528,8 @@ def _identity_items(U: int, N: int, dev, chunk: int, stream) -> object:
     eid = torch.arange(I, dtype=torch.int32, device=dev)
     val = torch.ones(I, dtype=torch.float32, device=dev)
     mask = torch.zeros(N, dtype=torch.uint8, device=dev)
-    mask[U:] = 1
+    a, b = rows if rows is not None else (0, I)
+    mask[U + a:U + b] = 1
     return CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, I, chunk, U, mask, stream), chunk)
 
 
@@ -569,6 +571,13 @@ class ReducePlan:
                                               self.dis, stream, items)
         self.partial.block_split = False
         self.identity = _identity_items(U, N, dev, self.chunk, stream)
+        # the last layer's item rows are reduce-scattered: this group's share of the items
+        # (I padded to a multiple of R; padding rows are zero partials that no pass writes)
+        R = shards.R
+        self.I_pad = -(-shards.I // R) * R
+        per = self.I_pad // R
+        self.share = (min(shards.I, self.g * per), min(shards.I, (self.g + 1) * per))
+        self.identity_share = _identity_items(U, N, dev, self.chunk, stream, self.share)
         self.n_sub = int(sel.sum().item())
         self.scratch = {}
 
@@ -593,11 +602,18 @@ class ReducePlan:
         N, U = self.shards.N, self.shards.U
         spmm(self.users, N, self.d, (x_items, x_items, U), e, acc, y, mode, div, mul, self._part(self.users, self.d))
 
-    def run_item_epilogue(self, v_items: torch.Tensor, e, acc, mode: int, div: float, mul: float) -> None:
+    def run_item_epilogue(self, v_items: torch.Tensor, e, acc, mode: int, div: float, mul: float,
+                          share: bool = False) -> None:
+        """v_items: the reduced item rows (all of them), or with share=True this group's share only
+        (row U + a of the share at v_items[0])."""
         from .propagate import spmm
 
         N, U = self.shards.N, self.shards.U
-        spmm(self.identity, N, self.d, (v_items, v_items, U), e, acc, None, mode, div, mul, None)
+        if share:
+            spmm(self.identity_share, N, self.d, (v_items, v_items, U + self.share[0]), e, acc, None, mode, div, mul,
+                 None)
+        else:
+            spmm(self.identity, N, self.d, (v_items, v_items, U), e, acc, None, mode, div, mul, None)
 
 
 class ItemReducer:
@@ -612,6 +628,30 @@ class ItemReducer:
         self.nccl = R > 1 and dist.get_backend(group) == "nccl"
         self.stream = None
         self.bytes = 0  # ring all_reduce traffic received per rank over the run
+
+    def start_scatter(self, buf: torch.Tensor, out: torch.Tensor, rank: int):
+        """out = this group member's 1/R row share of the sum of buf over the group (buf's rows a
+        multiple of R): reduce_scatter (nccl), or through host memory (gloo)."""
+        self.bytes += int((self.R - 1) / self.R * buf.numel() * buf.element_size())
+        if self.R == 1:
+            out.copy_(buf)
+            return None
+        if self.nccl:
+            if self.stream is None:
+                self.stream = torch.cuda.Stream(buf.device)
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(buf.device))
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ready)
+                self.dist.reduce_scatter_tensor(out, buf, op=self.dist.ReduceOp.SUM, group=self.group)
+                done = torch.cuda.Event()
+                done.record(self.stream)
+            return done
+        host = buf.cpu()
+        self.dist.all_reduce(host, op=self.dist.ReduceOp.SUM, group=self.group)
+        per = buf.shape[0] // self.R
+        out.copy_(host[rank * per:(rank + 1) * per])
+        return None
 
     def start(self, buf: torch.Tensor):
         self.bytes += int(2 * (self.R - 1) / self.R * buf.numel() * buf.element_size())
@@ -640,13 +680,15 @@ class ItemReducer:
 
 def propagate_forward_reduced(x0u: torch.Tensor, x0i: torch.Tensor, rplan, K: int,
                               reducer: ItemReducer) -> tuple[torch.Tensor, torch.Tensor]:
-    """(users [U, d], items [I, d]): the LightGCN final embedding of this row group's users (other
-    user rows unwritten) and of every item. x0u / x0i: the layer-0 tables (this rank's columns).
+    """(users [U, d], items [I, d]): the LightGCN final embedding of this row group's users and of
+    its share of the items, rplan.share = [a, b) (other rows unwritten). x0u / x0i: the layer-0
+    tables (this rank's columns).
 
     Layer k: the item partials from the users of layer k-1 (own rows), their all_reduce started;
     then the users of layer k from the items of layer k-1 (reduced one layer earlier); then, once
     layer k-1's reduction has landed, its item epilogue. Each reduction overlaps a user pass and
-    the next partial pass."""
+    the next partial pass. The last layer's partials are reduce-scattered (each group member gets
+    its share of the items: half a ring all_reduce's bytes) and only the share's epilogue runs."""
     U, d = x0u.shape
     I = x0i.shape[0]
     dev = x0u.device
@@ -657,7 +699,10 @@ def propagate_forward_reduced(x0u: torch.Tensor, x0i: torch.Tensor, rplan, K: in
     if K == 0:
         return (x0u / div) * mul, (x0i / div) * mul
     yu = [torch.empty((U, d), dtype=torch.float32, device=dev) for _ in range(min(2, K - 1))]
-    part = [torch.empty((I, d), dtype=torch.float32, device=dev) for _ in range(min(2, K))]
+    I_pad = getattr(rplan, "I_pad", I)
+    part = [torch.zeros((I_pad, d), dtype=torch.float32, device=dev) for _ in range(min(2, K))]
+    a, b = getattr(rplan, "share", (0, I))
+    share = torch.empty((I_pad // max(1, reducer.R), d), dtype=torch.float32, device=dev)
     e = (x0u, x0i, U)
     acc = (out_u, out_i, U)
 
@@ -674,7 +719,10 @@ def propagate_forward_reduced(x0u: torch.Tensor, x0i: torch.Tensor, rplan, K: in
         final = mode in (_ffi.EPI_FINAL_E, _ffi.EPI_FINAL_ACC)
         pk = part[(k - 1) % 2]
         rplan.run_partial(src_u, pk)
-        started = (reducer.start(pk), k)
+        if k < K:
+            started = (reducer.start(pk), k)
+        else:  # the last layer: this member's share of the item rows only
+            started = (reducer.start_scatter(pk, share, rplan.g), k)
         if pending is not None:  # layer k-1's items: reduced before this layer's users read them
             reducer.wait(pending[0], dev)
             m = mode_of(pending[1])
@@ -684,5 +732,6 @@ def propagate_forward_reduced(x0u: torch.Tensor, x0i: torch.Tensor, rplan, K: in
                         div if final else 1.0, mul if final else 1.0)
         pending = started
     reducer.wait(pending[0], dev)
-    rplan.run_item_epilogue(part[(K - 1) % 2], e, acc, mode_of(K), div, mul)
+    if b > a:
+        rplan.run_item_epilogue(share, e, acc, mode_of(K), div, mul, share=True)
     return out_u, out_i

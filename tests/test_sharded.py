@@ -231,6 +231,11 @@ class CpuReducePlan:
         sel = (ei[0] >= ua) & (ei[0] < ub)
         self.ei_sub, self.w_sub = ei[:, sel], self.w[sel]
         self.log = []
+        self.g = g
+        I = self.N - self.U
+        self.I_pad = -(-I // shards.R) * shards.R
+        per = self.I_pad // shards.R
+        self.share = (min(I, g * per), min(I, (g + 1) * per))
 
     @staticmethod
     def _epi(acc, e, rows, v, mode, div, mul):
@@ -249,21 +254,27 @@ class CpuReducePlan:
         self.log.append("partial")
         x = np.zeros((self.N, x_users.shape[1]), np.float32)
         x[:self.U] = x_users.numpy()
-        part_items[:] = torch.from_numpy(self.R.lgconv(x, self.ei_sub, self.w_sub)[self.U:])
+        part_items[:self.N - self.U] = torch.from_numpy(self.R.lgconv(x, self.ei_sub, self.w_sub)[self.U:])
 
     def run_users(self, x_items, e, acc, y, mode, div, mul):
         self.log.append("users")
         x = np.zeros((self.N, x_items.shape[1]), np.float32)
-        x[self.U:] = x_items.numpy()
+        x[self.U:] = x_items[:self.N - self.U].numpy()
         v = torch.from_numpy(self.R.lgconv(x, self.ei, self.w)[self.own])
         self._epi(acc[0], e[0] if e is not None else None, self.own, v, mode, div, mul)
         if y is not None and mode in (_ffi.EPI_INIT, _ffi.EPI_ADD):
             y[self.own] = v
 
-    def run_item_epilogue(self, v_items, e, acc, mode, div, mul):
+    def run_item_epilogue(self, v_items, e, acc, mode, div, mul, share=False):
         self.log.append("items")
-        rows = np.arange(self.N - self.U)
-        self._epi(acc[1], e[1], rows, v_items.clone(), mode, div, mul)
+        if share:
+            a, b = self.share
+            rows = np.arange(a, b)
+            v = v_items[:b - a].clone()
+        else:
+            rows = np.arange(self.N - self.U)
+            v = v_items[:self.N - self.U].clone()
+        self._epi(acc[1], e[1], rows, v, mode, div, mul)
 
 
 def _reduce_worker(rank, world, port, kind, K, out_dir, F=1):
@@ -290,8 +301,9 @@ def _reduce_worker(rank, world, port, kind, K, out_dir, F=1):
     ou, oi = propagate_forward_reduced(torch.from_numpy(uw[:, c0:c1].copy()), torch.from_numpy(iw[:, c0:c1].copy()),
                                        plan, K, red)
     ua, ub = shards.users(g)
+    a, b = plan.share
     np.save(os.path.join(out_dir, f"u{g}_{grid.col_group}.npy"), ou[ua:ub].numpy())
-    np.save(os.path.join(out_dir, f"i{rank}.npy"), oi.numpy())
+    np.save(os.path.join(out_dir, f"i{g}_{grid.col_group}.npy"), oi[a:b].numpy())
     np.save(os.path.join(out_dir, f"log{rank}.npy"), np.array(plan.log))
     dist.destroy_process_group()
 
@@ -299,10 +311,10 @@ def _reduce_worker(rank, world, port, kind, K, out_dir, F=1):
 @pytest.mark.parametrize("kind,world,K,F", [("sym", 2, 3, 1), ("sub", 2, 3, 1), ("hub", 3, 4, 1), ("sym", 4, 2, 2),
                                             ("sub", 4, 1, 1), ("hub", 2, 3, 1), ("sub", 8, 3, 2), ("sym", 2, 0, 1)])
 def test_reduce_mode_matches_oracle(tmp_path, kind, world, K, F):
-    """The reduce mode (users sharded, item rows all-reduced per layer) over gloo: every row group's
-    users and every rank's items within 1e-5 per row of the one-rank oracle forward (an item row is
-    the sum of R partial chains), the column groups' items identical across their row groups, and
-    the pass order of the overlapped schedule."""
+    """The reduce mode (users sharded, item rows all-reduced per layer, the last layer
+    reduce-scattered) over gloo: every row group's users and its share of the items within 1e-5
+    per row of the one-rank oracle forward (an item row is the sum of R partial chains), the
+    shares covering every item, and the pass order of the overlapped schedule."""
     import graphs
     from oracle import lgconv_ref as R
     from parity import assert_rows_close
@@ -321,12 +333,10 @@ def test_reduce_mode_matches_oracle(tmp_path, kind, world, K, F):
         ua, ub = shards.users(g)
         got = np.concatenate([np.load(tmp_path / f"u{g}_{c}.npy") for c in range(F)], axis=1)
         assert_rows_close(got, ref[ua:ub], what=f"users of row group {g}")
-    for r in range(world):
-        c = r % F
-        got = np.load(tmp_path / f"i{r}.npy")
-        assert_rows_close(got, ref[U:, c * w:(c + 1) * w], what=f"items on rank {r}")
-        same = np.load(tmp_path / f"i{c}.npy")
-        np.testing.assert_array_equal(got, same)
+    got_i = np.concatenate([np.concatenate([np.load(tmp_path / f"i{g}_{c}.npy") for c in range(F)], axis=1)
+                            for g in range(world // F)])
+    assert got_i.shape[0] == I  # the shares cover every item once
+    assert_rows_close(got_i, ref[U:], what="items (the row groups' shares)")
     if K:
         log = list(np.load(tmp_path / "log0.npy"))
         expect = ["partial", "users"] + ["partial", "items", "users"] * (K - 1) + ["items"]

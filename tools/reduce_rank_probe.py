@@ -28,6 +28,10 @@ class NoReduce:
         self.bytes += int(2 * (self.R - 1) / self.R * buf.numel() * buf.element_size())
         return None
 
+    def start_scatter(self, buf, out, rank):
+        self.bytes += int((self.R - 1) / self.R * buf.numel() * buf.element_size())
+        return None
+
     def wait(self, handle, device):
         pass
 
