@@ -691,7 +691,7 @@ def main():
         result["config"]["grid_trials_ms_per_step"] = grid_trials
     if exchange is not None:
         if st["mode"] == "reduce":
-            result["exchange"] = {"mode": "reduce", "all_reduces_per_step": K,
+            result["exchange"] = {"mode": "reduce", "all_reduces_per_step": K - 1, "reduce_scatters_per_step": 1,
                                   "MB_received_per_rank_per_step": exchange.bytes / args.steps / 1e6}
         else:
             result["exchange"] = {"mode": exchange.mode, "block_exchanges_per_step": 2 * (K - 1),
