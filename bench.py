@@ -812,7 +812,7 @@ def run_train(args):
         from lgcn_amd.train_step import FusedTrainStep
 
         fused = FusedTrainStep(model, opt, world=world if cols is None else 1,
-                               graphs=not args.no_graphs and not args.torch_adam and cols is None,
+                               graphs=not args.no_graphs and not args.torch_adam,
                                lazy=lazy, exchange=exchange, cols=cols,
                                neg_seed=(7 if cols is not None else 1000 + rank) if dp_mode != "replicated" else None)
 

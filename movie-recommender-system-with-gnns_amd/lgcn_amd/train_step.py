@@ -48,33 +48,96 @@ class ColumnGroup:
             raise ValueError(f"d={d_full} does not split into {world} column shares of a multiple of 4")
         self.world, self.rank, self.d_full, self.group = int(world), int(rank), int(d_full), group
         self.d = self.d_full // self.world
+        self._gathered = None  # every rank's norm partials (persistent: graph replays write it)
+        self.capture = None    # a _SegmentedGraph while a step is being captured
 
     @property
     def cols(self) -> tuple[int, int]:
         return self.rank * self.d, (self.rank + 1) * self.d
 
+    def _all_reduce(self, t: torch.Tensor) -> None:
+        import torch.distributed as dist
+
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
     def all_reduce(self, t: torch.Tensor) -> None:
-        import torch.distributed as dist
-
-        if self.world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-
-    def gather_partials(self, part: torch.Tensor) -> torch.Tensor:
-        import torch.distributed as dist
-
+        """t (this rank's [B, 6] partial sums) summed over the column groups, in place. While a
+        step is being captured, the capture is cut here and the all_reduce runs eagerly between
+        the graphs at replay."""
         if self.world == 1:
-            return part
-        out = torch.empty(self.world * part.numel(), dtype=part.dtype, device=part.device)
+            return
+        if self.capture is not None:
+            self.capture.split(lambda: self._all_reduce(t))
+            return
+        self._all_reduce(t)
+
+    def _gather(self, out: torch.Tensor, part: torch.Tensor) -> None:
+        import torch.distributed as dist
+
         if dist.get_backend(self.group) == "nccl":
             dist.all_gather_into_tensor(out, part, group=self.group)
         else:
             dist.all_gather(list(out.view(self.world, -1).unbind(0)), part, group=self.group)
+
+    def gather_partials(self, part: torch.Tensor) -> torch.Tensor:
+        """Every rank's norm partials in rank order (cut point of a capture, as all_reduce)."""
+        if self.world == 1:
+            return part
+        if self._gathered is None or self._gathered.numel() != self.world * part.numel():
+            if self.capture is not None:
+                raise RuntimeError("ColumnGroup: take one eager step before capturing (norm partials buffer)")
+            self._gathered = torch.empty(self.world * part.numel(), dtype=part.dtype, device=part.device)
+        out = self._gathered
+        if self.capture is not None:
+            self.capture.split(lambda: self._gather(out, part))
+        else:
+            self._gather(out, part)
         return out
 
     def reg_coeff(self, coeff: float) -> float:
         """The coefficient whose kreg = c * 2 / (B * d) over this rank's d columns equals the full
         width's coeff * 2 / (B * d_full) (the reg rows the scatters form, RegSrc)."""
         return float(np.float32(float(coeff) * self.d / self.d_full))
+
+
+class _SegmentedGraph:
+    """A training step captured as hipGraphs cut at its eager collectives (column-sharded
+    training: the [B, 6] all_reduce and the norm partials' all_gather): replay() runs graph 0,
+    collective 0, graph 1, ... in capture order. The graphs share one private memory pool, which
+    is safe because they always replay in the order they were captured."""
+
+    def __init__(self):
+        self.graphs, self.colls = [], []
+        self.pool = torch.cuda.graph_pool_handle()
+
+    def _begin(self) -> None:
+        g = torch.cuda.CUDAGraph()
+        g.capture_begin(pool=self.pool)
+        self.graphs.append(g)
+
+    def split(self, collective) -> None:
+        self.graphs[-1].capture_end()
+        self.colls.append(collective)
+        self._begin()
+
+    def capture(self, fn):
+        torch.cuda.synchronize()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self._begin()
+            try:
+                out = fn()
+            finally:
+                self.graphs[-1].capture_end()
+        torch.cuda.current_stream().wait_stream(side)
+        return out
+
+    def replay(self) -> None:
+        for i, g in enumerate(self.graphs):
+            g.replay()
+            if i < len(self.colls):
+                self.colls[i]()
 
 
 class _BatchState:
@@ -249,7 +312,8 @@ class FusedTrainStep:
         neg_seed: draw step k's negatives from a generator seeded (neg_seed, k) instead of the
         global CUDA generator (the same draws whichever exchange runs, and whenever they are drawn).
         cols (lazy): column-sharded training — the model holds this rank's ColumnGroup columns,
-        every rank steps the same batches with the same negatives (the same neg_seed); eager."""
+        every rank steps the same batches with the same negatives (the same neg_seed); with graphs,
+        each batch's step is captured as graphs cut at the two collectives (_SegmentedGraph)."""
         self.model = model
         self.optimizer = optimizer
         self.coeff = float(bpr_coeff)
@@ -272,8 +336,8 @@ class FusedTrainStep:
 
         self.cols = cols
         if cols is not None:
-            if not lazy or exchange is not None or graphs:
-                raise ValueError("cols= needs lazy=True (RowLazyAdam), no exchange and graphs=False")
+            if not lazy or exchange is not None:
+                raise ValueError("cols= needs lazy=True (RowLazyAdam) and no exchange")
             if model.dim_h != cols.d:
                 raise ValueError(f"the model holds {model.dim_h} columns, the ColumnGroup share is {cols.d}")
         self.owner = isinstance(exchange, OwnerExchange)
@@ -637,7 +701,15 @@ class FusedTrainStep:
                 torch.cuda.synchronize()
                 steps = self.optimizer.steps
                 g = torch.cuda.CUDAGraph()
-                if self.exchange is None:
+                if self.cols is not None and self.cols.world > 1:
+                    # graphs cut at the column groups' two collectives, which run eagerly between them
+                    g = _SegmentedGraph()
+                    self.cols.capture = g
+                    try:
+                        st.graph_loss = g.capture(lambda: self._step_lazy(st, draw=False))
+                    finally:
+                        self.cols.capture = None
+                elif self.exchange is None:
                     with torch.cuda.graph(g):
                         st.graph_loss = self._step_lazy(st, draw=False)
                 else:  # two halves: the all_gather between them runs eagerly

@@ -1,7 +1,8 @@
 """One rank of the data-parallel training check in tests/test_gpu_exchange.py (started as a
-child process per rank; gloo over one GPU): trains the same Cluster-GCN batches three ways —
-dense FusedAdam after an all_reduce of both gradients, and the row-lazy Adam with the
-row-sparse exchange (eager and hipGraph-replayed) — and saves the final tables and losses.
+child process per rank; gloo over one GPU): trains the same Cluster-GCN batches several ways —
+dense FusedAdam after an all_reduce of both gradients, the row-lazy Adam with the row-sparse
+exchange or the owner-sharded exchange, and column-sharded (DP_VARIANTS cols / cols_graphs), each
+eager and hipGraph-replayed — and saves the final tables and losses.
 
 python tests/dp_exchange_worker.py RANK WORLD PORT OUT CLIP [BATCHES.npz]
 
@@ -63,9 +64,19 @@ def main():
     steps = int(os.environ.get("DP_STEPS", "12"))
     for name in variants:
         torch.manual_seed(0)
-        m = LightGCN(U, I, num_layers=3, dim_h=d).to(gpu)
+        cg = None
+        if name.startswith("cols"):
+            # column-sharded: every rank steps the same batches on its d / W columns
+            from lgcn_amd.train_step import ColumnGroup
+
+            cg = ColumnGroup(world, rank, d)
+        m = LightGCN(U, I, num_layers=3, dim_h=d if cg is None else cg.d).to(gpu)
         ex = None
-        if name == "dense":
+        if cg is not None:
+            opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-2,
+                              max_grad_norm=clip_)
+            step = FusedTrainStep(m, opt, lazy=True, cols=cg, graphs=name.endswith("_graphs"), neg_seed=7)
+        elif name == "dense":
             opt = FusedAdam(m.parameters(), lr=1e-2, max_grad_norm=clip_, capturable=True)
             step = FusedTrainStep(m, opt, world=world, neg_seed=100 + rank)
         else:
@@ -79,7 +90,8 @@ def main():
                                   neg_seed=100 + rank)  # per-rank negatives, the same for every variant
         losses = []
         for i in range(steps):
-            b = batches[share[i % len(share)]]
+            order = share if cg is None else list(range(len(batches)))
+            b = batches[order[i % len(order)]]
             if name.startswith("owner"):
                 nxt = batches[share[(i + 1) % len(share)]] if i + 1 < steps else None
                 losses.append(step.step(b, nxt).item())
