@@ -9,11 +9,15 @@ embedding tables resident in HBM. value = K * E / wall time per step: ONE graph 
 Multi-GPU: `python bench.py --gpus N` starts N rank processes itself (one per GPU; under
 torchrun, which sets WORLD_SIZE, it is one of them). Strong scaling. C2 is sharded over an R x F
 grid (lgcn_amd.sharded): F column groups (each propagates d/F columns, no exchange between them)
-times R row groups (each rank propagates its own edge-balanced destination rows of the same
-graph, and each layer's two output blocks (user rows, item rows) are all-gathered over RCCL within
-the column group on a side stream while the other half-layer computes). With R = 1 a rank's
-columns are bitwise the 1-GPU result; with R > 1 ranks run the plain schedule at chunk 128, whose
-rows are within 1e-5 of the sliced 1-GPU result (bitwise the 1-GPU plain schedule at that chunk).
+times R row groups, in one of three exchange modes timed per grid: allgather / p2p (each rank
+propagates its own edge-balanced destination rows of the same graph, and each layer's two output
+blocks (user rows, item rows) are all-gathered, or sent peer to peer, over RCCL within the column
+group on a side stream while the other half-layer computes) and reduce (users sharded, every rank
+sums its users' share of every item row; the item partials are all-reduced per layer, the last
+layer reduce-scattered). With R = 1 a rank's columns are bitwise the 1-GPU result; with R > 1
+ranks run the plain schedule at chunk 128, whose rows are within 1e-5 of the sliced 1-GPU result
+(allgather / p2p: bitwise the 1-GPU plain schedule at that chunk; reduce: an item row is the sum
+of R partial chains).
 C5 (--config c5) is feature-sharded: d/N columns per rank, no collective. The barrier and the
 max-over-ranks time go over RCCL.
 
