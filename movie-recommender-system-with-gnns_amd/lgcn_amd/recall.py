@@ -123,11 +123,47 @@ def legacy_choice(n: int, size: int, draws: int) -> np.ndarray:
     return out
 
 
-def compute_recall_at_k(embs, k: int = 20, num_samples: int = 10, sample_size: int = 100) -> float:
-    """The reference's compute_recall_at_k (utils/train_test.py:165-212) on device tensors."""
+class _Picks:
+    """legacy_choice on a host thread (the C++ call releases the GIL), so the draws overlap GPU
+    work the caller issues meanwhile — which must not use numpy's global generator."""
+
+    def __init__(self, n: int, size: int, draws: int):
+        import threading
+
+        self.args, self.out, self.err = (n, size, draws), None, None
+        self.thread = threading.Thread(target=self._run, daemon=True)
+        self.thread.start()
+
+    def _run(self):
+        try:
+            self.out = legacy_choice(*self.args)
+        except BaseException as e:  # noqa: BLE001 — re-raised in result()
+            self.err = e
+
+    def result(self) -> np.ndarray:
+        self.thread.join()
+        if self.err is not None:
+            raise self.err
+        return self.out
+
+
+def start_picks(n: int, sample_size: int = 100, num_samples: int = 10) -> _Picks:
+    """Start compute_recall_at_k's user draws (numpy's, in the reference's order) in the background."""
+    return _Picks(n, sample_size, num_samples)
+
+
+def compute_recall_at_k(embs, k: int = 20, num_samples: int = 10, sample_size: int = 100,
+                        picks: _Picks | None = None) -> float:
+    """The reference's compute_recall_at_k (utils/train_test.py:165-212) on device tensors.
+    picks: the draws already started by start_picks(users, sample_size, num_samples)."""
     user_embs, pos_item_embs, neg_item_embs = embs
     num_pos = pos_item_embs.size(0)
-    picked = legacy_choice(user_embs.size(0), sample_size, num_samples).reshape(-1)
+    if picks is not None:
+        if picks.args != (user_embs.size(0), sample_size, num_samples):
+            raise ValueError(f"recall: picks were started for {picks.args}")
+        picked = picks.result().reshape(-1)
+    else:
+        picked = legacy_choice(user_embs.size(0), sample_size, num_samples).reshape(-1)
     hits = topk_hits(user_embs, torch.from_numpy(picked), pos_item_embs, neg_item_embs, k)
     if int(hits.min().item()) < 0:
         raise RuntimeError("recall: a query ranked fewer than k candidates")

@@ -89,15 +89,16 @@ def train(model: torch.nn.Module, optimizer: torch.optim.Optimizer, train_loader
     return total_loss.item() / total_w
 
 
-def compute_recall_at_k(embs, k: int = 20, num_samples: int = 10, sample_size: int = 100) -> float:
+def compute_recall_at_k(embs, k: int = 20, num_samples: int = 10, sample_size: int = 100, picks=None) -> float:
     """Reference Recall@k (:165-212): sample_size random positive-edge rows as 'users', score
     them against every positive and negative row of the batch, count top-k hits among the
-    positives, divide by the number of positives; mean over num_samples draws."""
+    positives, divide by the number of positives; mean over num_samples draws. picks (device
+    path): the draws already started by lgcn_amd.recall.start_picks."""
     user_embs, pos_item_embs, neg_item_embs = embs
     if user_embs.is_cuda:  # HIP path: f32 MFMA scores + per-user top-k selection, no score matrix
         from lgcn_amd.recall import compute_recall_at_k as recall_hip
 
-        return recall_hip(embs, k=k, num_samples=num_samples, sample_size=sample_size)
+        return recall_hip(embs, k=k, num_samples=num_samples, sample_size=sample_size, picks=picks)
     num_pos = pos_item_embs.size(0)
     candidates = torch.cat((normalize_embedding(pos_item_embs), normalize_embedding(neg_item_embs))).t()
     per_sample = []
@@ -120,8 +121,15 @@ def evaluate(model: torch.nn.Module, test_data, device, top_k: int = 100):
     with torch.no_grad():
         test_data = test_data.to(device)
         embs = compute_embeddings(model, test_data, device)
+        picks = None
+        if embs[1].is_cuda:
+            # numpy's user draws for Recall@k (host) overlap the loss (GPU); neither touches the
+            # other's generator, so the draws and the loss are the sequential ones
+            from lgcn_amd.recall import start_picks
+
+            picks = start_picks(embs[1].size(0))
         test_loss = bpr_loss(*embs).item()
-        recall_at_k = compute_recall_at_k((embs[1], embs[3], embs[5]), k=top_k)
+        recall_at_k = compute_recall_at_k((embs[1], embs[3], embs[5]), k=top_k, picks=picks)
     return test_loss, recall_at_k
 
 

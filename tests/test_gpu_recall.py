@@ -126,3 +126,36 @@ def test_compute_recall_at_k_matches_oracle_at_scale(gpu):
     bound = unseparated / (pos.shape[0] * 100 * len(detail))
     assert abs(got - ref) <= bound + 1e-6 * abs(ref)
     print(f"recall@100 {got:.6f} vs oracle {ref:.6f}; unseparated queries {unseparated} of {100 * len(detail)}")
+
+
+def test_evaluate_overlapped_draws_equal_sequential(gpu):
+    """evaluate() on the device starts numpy's Recall user draws on a host thread while the loss
+    runs (lgcn_amd.recall.start_picks): same loss, same Recall and same numpy state afterwards as
+    the sequential compute_embeddings -> bpr_loss -> compute_recall_at_k."""
+    import graphs
+    from models.light_gcn import LightGCN
+    from utils import train_test as TT
+
+    U, I, ei = graphs.subsampled(U=3000, I=1500, pairs=20000, seed=5)
+
+    class _B:
+        edge_index = torch.from_numpy(ei).to(gpu)
+
+        def to(self, _):
+            return self
+
+    torch.manual_seed(0)
+    model = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
+    torch.manual_seed(42)
+    np.random.seed(43)
+    loss_a, rec_a = TT.evaluate(model, _B(), gpu, top_k=100)
+    state_a = np.random.get_state()
+    torch.manual_seed(42)
+    np.random.seed(43)
+    with torch.no_grad():
+        embs = TT.compute_embeddings(model, _B(), gpu)
+        loss_b = TT.bpr_loss(*embs).item()
+        rec_b = TT.compute_recall_at_k((embs[1], embs[3], embs[5]), k=100)
+    state_b = np.random.get_state()
+    assert loss_a == loss_b and rec_a == rec_b
+    assert state_a[2] == state_b[2] and np.array_equal(state_a[1], state_b[1])
