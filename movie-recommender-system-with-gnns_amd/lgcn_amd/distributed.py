@@ -16,8 +16,21 @@ the union of the ranks' rows.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
+
+
+def device_collectives(group=None) -> bool:
+    """True where the multi-GPU paths run their collectives on device tensors in stream order
+    (backend "nccl" = RCCL): side streams, events, in-place views, no host staging. gloo runs the
+    same calls on CUDA tensors too (tools/rccl_probe.py --backend gloo), so LGCN_DEVICE_COLLECTIVES=1
+    sends a gloo run down that branch — how the ranks-on-one-GPU tests exercise the code the RCCL
+    runs take, since RCCL refuses two ranks on one GPU."""
+    if os.environ.get("LGCN_DEVICE_COLLECTIVES") == "1":
+        return True
+    return dist.get_backend(group) == "nccl"
 
 
 def world_info():
@@ -65,7 +78,7 @@ def exchange_capacity(batches, num_users: int) -> int:
     world, _ = world_info()
     if world > 1:
         t = torch.tensor([cap], dtype=torch.int64)
-        if dist.get_backend() == "nccl":
+        if device_collectives():
             t = t.cuda()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         cap = int(t.item())
@@ -112,7 +125,7 @@ class RowExchange:
         self.bytes += (self.world - 1) * self.blk * 4
         if self.world == 1:
             self.pack_all.copy_(self.pack)
-        elif dist.get_backend() == "nccl":
+        elif device_collectives():
             dist.all_gather_into_tensor(self.pack_all, self.pack)
         else:
             dist.all_gather(list(self.pack_all.view(self.world, self.blk).unbind(0)), self.pack)

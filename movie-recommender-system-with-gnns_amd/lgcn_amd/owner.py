@@ -37,6 +37,7 @@ import torch
 import torch.distributed as dist
 
 from . import _ffi
+from .distributed import device_collectives
 
 
 def owner_capacity(batches, num_users: int, world: int, slack: float = 1.25, floor: int = 64) -> int:
@@ -53,7 +54,7 @@ def owner_capacity(batches, num_users: int, world: int, slack: float = 1.25, flo
         cap = max(cap, int(per_owner) + int(np.ceil(B / world * slack)) + floor)
     if dist.is_available() and dist.is_initialized() and world > 1:
         t = torch.tensor([cap], dtype=torch.int64)
-        if dist.get_backend() == "nccl":
+        if device_collectives():
             t = t.cuda()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         cap = int(t.item())
@@ -93,7 +94,7 @@ class OwnerExchange:
         self.norm_parts = int(norm_parts)
         self.partials = torch.zeros(self.norm_parts, dtype=torch.float32, device=device)
         self.partials_all = torch.zeros(W * self.norm_parts, dtype=torch.float32, device=device)
-        self.nccl = W > 1 and dist.get_backend() == "nccl"
+        self.nccl = W > 1 and device_collectives()
         self.bytes = 0  # received from peers over the run (self blocks excluded)
         self.pending = None  # the batch state whose rows the last step requested
 

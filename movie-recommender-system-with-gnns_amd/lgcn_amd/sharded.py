@@ -41,6 +41,7 @@ import numpy as np
 import torch
 
 from . import _ffi
+from .distributed import device_collectives
 
 ROW_COST = 4  # a row's epilogue (acc/e/y traffic) costs about as much as this many gathered edges
 
@@ -370,7 +371,7 @@ class BlockExchange:
         self.members = list(members) if members is not None else list(range(shards.W))
         if len(self.members) != shards.W:
             raise ValueError(f"{len(self.members)} exchange members for {shards.W} row groups")
-        self.nccl = dist.get_backend(group) == "nccl"
+        self.nccl = device_collectives(group)
         self.stream = None
         self.bytes = 0  # received per rank, over the run
 
@@ -625,7 +626,7 @@ class ItemReducer:
         import torch.distributed as dist
 
         self.dist, self.R, self.group = dist, int(R), group
-        self.nccl = R > 1 and dist.get_backend(group) == "nccl"
+        self.nccl = R > 1 and device_collectives(group)
         self.stream = None
         self.bytes = 0  # ring all_reduce traffic received per rank over the run
 

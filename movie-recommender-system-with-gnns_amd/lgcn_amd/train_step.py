@@ -74,7 +74,9 @@ class ColumnGroup:
     def _gather(self, out: torch.Tensor, part: torch.Tensor) -> None:
         import torch.distributed as dist
 
-        if dist.get_backend(self.group) == "nccl":
+        from .distributed import device_collectives
+
+        if device_collectives(self.group):
             dist.all_gather_into_tensor(out, part, group=self.group)
         else:
             dist.all_gather(list(out.view(self.world, -1).unbind(0)), part, group=self.group)

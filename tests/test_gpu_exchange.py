@@ -206,12 +206,13 @@ def _check_owner_vs_replicated(res, clip):
             assert abs(a - b) <= 1e-5 * max(1.0, abs(a))
 
 
-def _spawn(world, tmp_path, clip, variants, steps=12, npz=None, timeout=300):
+def _spawn(world, tmp_path, clip, variants, steps=12, npz=None, timeout=300, device_collectives=False):
     port = str(_free_port())
     worker = str(ROOT / "tests" / "dp_exchange_worker.py")
-    outs = [str(tmp_path / f"w{world}_r{r}.pt") for r in range(world)]
+    tag = "dc" if device_collectives else "h"
+    outs = [str(tmp_path / f"w{world}_{tag}_r{r}.pt") for r in range(world)]
     env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", DP_VARIANTS=variants, DP_STEPS=str(steps),
-               OMP_NUM_THREADS="1")
+               OMP_NUM_THREADS="1", LGCN_DEVICE_COLLECTIVES="1" if device_collectives else "0")
     extra = [npz] if npz else []
     procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), str(world), port, outs[r], str(clip), *extra],
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
@@ -261,3 +262,20 @@ def test_column_sharded_graph_replay_matches_eager(gpu, tmp_path, world, clip):
         assert torch.equal(eager["user"], graphs["user"]) and torch.equal(eager["item"], graphs["item"]), r
         if r:
             assert eager["losses"] == res[0]["cols"]["losses"]  # every rank computes the full-width loss
+
+
+@pytest.mark.parametrize("clip", [float("inf"), 1.0])
+def test_dp_exchanges_device_collectives_equal_host_path(gpu, tmp_path, clip):
+    """Four ranks (gloo, one GPU) down the RCCL branches (LGCN_DEVICE_COLLECTIVES=1: RowExchange's
+    all_gather_into_tensor, OwnerExchange's all_to_all_single / all_gather on CUDA tensors,
+    ColumnGroup's device all_gather; the capacity all_reduces on device) == the same run through
+    host memory, bitwise, for the replicated, owner-sharded and column-sharded modes (eager and
+    graphs)."""
+    variants = "lazy,lazy_graphs,owner,owner_graphs,cols,cols_graphs"
+    host = _spawn(4, tmp_path, clip, variants, steps=12)
+    dev = _spawn(4, tmp_path, clip, variants, steps=12, device_collectives=True)
+    for r in range(4):
+        for name in variants.split(","):
+            assert host[r][name]["losses"] == dev[r][name]["losses"], (r, name)
+            assert torch.equal(host[r][name]["user"], dev[r][name]["user"]), (r, name)
+            assert torch.equal(host[r][name]["item"], dev[r][name]["item"]), (r, name)

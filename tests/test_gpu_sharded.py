@@ -114,7 +114,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, case, out_dir, F=1, mode="allgather"):
+def _worker(rank, world, port, case, out_dir, F=1, mode="allgather", dc=False):
     import sys
 
     from conftest import PKG, ROOT
@@ -124,6 +124,8 @@ def _worker(rank, world, port, case, out_dir, F=1, mode="allgather"):
     slice_mb = CASES[case][4]
     if slice_mb:
         os.environ["LGCN_SLICE_MB"] = slice_mb
+    if dc:  # the RCCL branch's code (side stream, events, in-place device collectives) over gloo
+        os.environ["LGCN_DEVICE_COLLECTIVES"] = "1"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -148,13 +150,26 @@ def test_sharded_ranks_bitwise(gpu, monkeypatch, tmp_path, case, world, F, mode)
     output is bitwise the one-GPU forward with the schedule the ranks run (R = 1: each column share
     at its width; R > 1: lgcn_amd.sharded.rank_chunk at the full width); with R > 1 also within
     1e-5 per row of the default one."""
+    _check_sharded_ranks(gpu, monkeypatch, tmp_path, case, world, F, mode, False)
+
+
+@pytest.mark.parametrize("case,world,F,mode", [("ml25m5_sliced", 4, 2, "allgather"), ("hub_sliced", 4, 2, "p2p"),
+                                               ("ml25m5_plain", 3, 1, "p2p"), ("sub_K2_d128", 2, 1, "allgather")])
+def test_sharded_ranks_device_collectives(gpu, monkeypatch, tmp_path, case, world, F, mode):
+    """The same, down the RCCL branch of BlockExchange (LGCN_DEVICE_COLLECTIVES=1: in-place
+    all_gather_into_tensor / batch_isend_irecv on CUDA tensors, on a side stream the compute
+    stream waits on through events), with gloo carrying the bytes: bitwise the one-GPU forward."""
+    _check_sharded_ranks(gpu, monkeypatch, tmp_path, case, world, F, mode, True)
+
+
+def _check_sharded_ranks(gpu, monkeypatch, tmp_path, case, world, F, mode, dc):
     slice_mb = CASES[case][4]
     if slice_mb:
         monkeypatch.setenv("LGCN_SLICE_MB", slice_mb)
     R = world // F
     U, I, ei, uw, iw, ref, sched, n_hubs = _reference(gpu, case, R, F)
     torch.cuda.synchronize()
-    mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path), F, mode), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path), F, mode, dc), nprocs=world, join=True)
     got_u = np.concatenate([np.concatenate([np.load(tmp_path / f"u{r}_{c}.npy") for c in range(F)], axis=1)
                             for r in range(R)])
     got_i = np.concatenate([np.concatenate([np.load(tmp_path / f"i{r}_{c}.npy") for c in range(F)], axis=1)
@@ -171,12 +186,15 @@ def test_sharded_ranks_bitwise(gpu, monkeypatch, tmp_path, case, world, F, mode)
     assert sum(int(m[0]) for m in meta) == n_hubs
 
 
-def _reduce_worker(rank, world, port, case, out_dir, F=1):
+def _reduce_worker(rank, world, port, case, out_dir, F=1, dc=False):
     import sys
 
     from conftest import PKG, ROOT
     sys.path[:0] = [str(PKG), str(ROOT), str(ROOT / "tests")]
     import torch.distributed as dist
+
+    if dc:
+        os.environ["LGCN_DEVICE_COLLECTIVES"] = "1"
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -210,6 +228,17 @@ def test_reduce_mode_ranks_match_oracle(gpu, tmp_path, case, world, F):
     """The reduce mode with the HIP kernels (gloo, every rank on the one GPU): users of every row
     group and every row group's share of the items (the last layer reduce-scattered) within 1e-5
     per row of the C oracle forward; the shares cover every item."""
+    _check_reduce_ranks(gpu, tmp_path, case, world, F, False)
+
+
+@pytest.mark.parametrize("case,world,F", [("ml25m5_plain", 4, 2), ("ml25m5_sliced", 8, 2), ("hub_sliced", 3, 1)])
+def test_reduce_mode_device_collectives(gpu, tmp_path, case, world, F):
+    """The same down ItemReducer's RCCL branch (LGCN_DEVICE_COLLECTIVES=1: all_reduce and the last
+    layer's reduce_scatter_tensor on CUDA tensors, side stream + events), gloo carrying the bytes."""
+    _check_reduce_ranks(gpu, tmp_path, case, world, F, True)
+
+
+def _check_reduce_ranks(gpu, tmp_path, case, world, F, dc):
     import graphs
     from oracle import c_oracle
     from parity import assert_rows_close
@@ -221,7 +250,7 @@ def test_reduce_mode_ranks_match_oracle(gpu, tmp_path, case, world, F):
     uw, iw = graphs.embeddings(U, I, d, seed=K + d)
     ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
     torch.cuda.synchronize()
-    mp.spawn(_reduce_worker, args=(world, _free_port(), case, str(tmp_path), F), nprocs=world, join=True)
+    mp.spawn(_reduce_worker, args=(world, _free_port(), case, str(tmp_path), F, dc), nprocs=world, join=True)
     R = world // F
     shards = UserShards.build(np.bincount(ei[1], minlength=U + I), U, R)
     w = d // F
