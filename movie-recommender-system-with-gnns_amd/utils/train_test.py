@@ -128,8 +128,12 @@ def evaluate(model: torch.nn.Module, test_data, device, top_k: int = 100):
             from lgcn_amd.recall import start_picks
 
             picks = start_picks(embs[1].size(0))
-        test_loss = bpr_loss(*embs).item()
-        recall_at_k = compute_recall_at_k((embs[1], embs[3], embs[5]), k=top_k, picks=picks)
+        try:
+            test_loss = bpr_loss(*embs).item()
+            recall_at_k = compute_recall_at_k((embs[1], embs[3], embs[5]), k=top_k, picks=picks)
+        finally:
+            if picks is not None:  # never leave the draws moving numpy's state after we return
+                picks.thread.join()
     return test_loss, recall_at_k
 
 
