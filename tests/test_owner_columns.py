@@ -111,3 +111,26 @@ def test_column_group_collectives_world2(tmp_path):
         res = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
         assert torch.equal(res["sum"], torch.full((6,), 3.0))
         assert res["parts"].tolist() == [0, 1, 2, 3, 10, 11, 12, 13]
+
+
+def _dc_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lgcn_amd.distributed import device_collectives
+
+    plain = device_collectives()
+    os.environ["LGCN_DEVICE_COLLECTIVES"] = "1"
+    forced = device_collectives()
+    os.environ.pop("LGCN_DEVICE_COLLECTIVES")
+    torch.save({"plain": plain, "forced": forced}, os.path.join(out, f"dc{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_device_collectives_switch(tmp_path):
+    """device_collectives(): False on a gloo group, True with LGCN_DEVICE_COLLECTIVES=1 (how the
+    GPU tests send gloo runs down the RCCL branches)."""
+    mp.spawn(_dc_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        res = torch.load(tmp_path / f"dc{r}.pt", weights_only=True)
+        assert res == {"plain": False, "forced": True}
