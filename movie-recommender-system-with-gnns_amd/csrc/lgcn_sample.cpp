@@ -12,11 +12,13 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
+#include <exception>
 #include <thread>
 #include <vector>
 
-#include "lgcn.h"
+#include "lgcn_common.h"
+
+using lgcn::fail;
 
 namespace {
 
@@ -203,25 +205,25 @@ extern "C" int lgcn_legacy_choice(uint32_t* key, int32_t* pos, int64_t n, int64_
         std::vector<int32_t> x(static_cast<size_t>(n) + 1);
         for (int64_t d = 0; d < draws; ++d) one_choice(g, n, size, x.data(), out + d * size);
     } else {
-        // per-slot scratch kept across calls (first-touching 4n bytes per worker per call costs
-        // page faults comparable to a shuffle); one call at a time uses it
-        static std::mutex lock;
-        static std::vector<std::vector<int32_t>> xs;
-        std::lock_guard<std::mutex> hold(lock);
-        if (xs.size() < static_cast<size_t>(T)) xs.resize(static_cast<size_t>(T));
+        std::vector<std::vector<int32_t>> xs(static_cast<size_t>(T));  // one scratch per worker slot
         std::vector<std::thread> workers;
-        workers.reserve(static_cast<size_t>(draws));
-        for (int64_t d = 0; d < draws; ++d) {
-            if (static_cast<int64_t>(workers.size()) >= T) workers[static_cast<size_t>(d - T)].join();
-            // a worker slot is reused once the draw that held it has been joined
-            std::vector<int32_t>* x = &xs[static_cast<size_t>(d % T)];
-            workers.emplace_back([g, n, size, x, o = out + d * size]() mutable {
-                x->resize(static_cast<size_t>(n) + 1);
-                one_choice(g, n, size, x->data(), o);
-            });
-            skip_shuffle(g, n);
+        try {
+            workers.reserve(static_cast<size_t>(draws));
+            for (auto& x : xs) x.resize(static_cast<size_t>(n) + 1);
+            for (int64_t d = 0; d < draws; ++d) {
+                if (static_cast<int64_t>(workers.size()) >= T) workers[static_cast<size_t>(d - T)].join();
+                // a worker slot is reused once the draw that held it has been joined
+                int32_t* x = xs[static_cast<size_t>(d % T)].data();
+                workers.emplace_back([g, n, size, x, o = out + d * size]() mutable { one_choice(g, n, size, x, o); });
+                skip_shuffle(g, n);
+            }
+        } catch (const std::exception& e) {  // no thread / no memory: the caller's state is untouched
+            for (auto& w : workers)
+                if (w.joinable()) w.join();
+            return fail(LGCN_E_UNSUPPORTED, "lgcn_legacy_choice: %s", e.what());
         }
-        for (int64_t d = draws > T ? draws - T : 0; d < draws; ++d) workers[static_cast<size_t>(d)].join();
+        for (auto& w : workers)
+            if (w.joinable()) w.join();
     }
     std::memcpy(key, g.mt, sizeof(g.mt));
     *pos = g.pos;

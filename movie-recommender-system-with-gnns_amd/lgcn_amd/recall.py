@@ -117,8 +117,10 @@ def legacy_choice(n: int, size: int, draws: int) -> np.ndarray:
     key = np.array(state[1], dtype=np.uint32)
     pos = ctypes.c_int32(int(state[2]))
     out = np.empty((draws, size), dtype=np.int64)
-    _ffi.check(_ffi.load().lgcn_legacy_choice(key.ctypes.data, ctypes.byref(pos), n, size, draws, out.ctypes.data),
-               "lgcn_legacy_choice")
+    rc = _ffi.load().lgcn_legacy_choice(key.ctypes.data, ctypes.byref(pos), n, size, draws, out.ctypes.data)
+    if rc == _ffi.E_UNSUPPORTED:  # no worker thread / memory: numpy's own draws (the state is untouched)
+        return np.stack([np.random.choice(n, size, replace=False) for _ in range(draws)])
+    _ffi.check(rc, "lgcn_legacy_choice")
     np.random.set_state(("MT19937", key, pos.value, state[3], state[4]))
     return out
 
