@@ -202,13 +202,15 @@ def test_grid_candidates():
     assert grid_candidates(1, 64) == [(1, 1, None)]
     assert grid_candidates(2, 64) == [(1, 2, None)]
     # world >= 4: R - 1 >= 3 links; "reduce" (users sharded, items all-reduced) for every R > 1
-    rows_only = lambda w: [(w, 1, "allgather"), (w, 1, "p2p"), (w, 1, "reduce")]  # noqa: E731
-    assert grid_candidates(4, 64) == [(1, 4, None), (2, 2, "allgather"), (2, 2, "reduce")] + rows_only(4)
+    # peer sends (p2p) are timed after every other candidate (a hang there cannot stop the others)
+    rows_only = lambda w: [(w, 1, "allgather"), (w, 1, "reduce")]  # noqa: E731
+    assert grid_candidates(4, 64) == [(1, 4, None), (2, 2, "allgather"), (2, 2, "reduce")] + rows_only(4) + \
+        [(4, 1, "p2p")]
     assert grid_candidates(8, 64) == [(1, 8, None), (2, 4, "allgather"), (2, 4, "reduce"), (4, 2, "allgather"),
-                                      (4, 2, "p2p"), (4, 2, "reduce")] + rows_only(8)
-    assert grid_candidates(3, 64) == rows_only(3)   # odd world: rows only
-    assert grid_candidates(8, 32) == [(2, 4, "allgather"), (2, 4, "reduce"), (4, 2, "allgather"), (4, 2, "p2p"),
-                                      (4, 2, "reduce")] + rows_only(8)  # 4-col shares: no
+                                      (4, 2, "reduce")] + rows_only(8) + [(4, 2, "p2p"), (8, 1, "p2p")]
+    assert grid_candidates(3, 64) == rows_only(3) + [(3, 1, "p2p")]   # odd world: rows only
+    assert grid_candidates(8, 32) == [(2, 4, "allgather"), (2, 4, "reduce"), (4, 2, "allgather"),
+                                      (4, 2, "reduce")] + rows_only(8) + [(4, 2, "p2p"), (8, 1, "p2p")]  # 4-col shares: no
     assert (4, 1, "reduce") not in grid_candidates(4, 64, bipartite=False)
     for R, F, _ in grid_candidates(8, 256):
         assert R * F == 8 and (256 // F) % 4 == 0
