@@ -191,8 +191,8 @@ def grid_candidates(world: int, d: int, bipartite: bool = True) -> list[tuple[in
     if any(F > 1 for _, F, _ in out) and world < 4:
         out = [c for c in out if c[1] > 1]
     # the peer-send candidates last: batch_isend_irecv is the one exchange outside RCCL's plain
-    # collectives, and a collective that hangs (rather than raises) ends the whole timed choice —
-    # every other candidate has been timed by then
+    # collectives, so the log holds every plain candidate's time before them (a candidate that
+    # raises is skipped either way; one that hangs ends the run at the process-group timeout)
     return [c for c in out if c[2] != "p2p"] + [c for c in out if c[2] == "p2p"]
 
 
