@@ -38,7 +38,7 @@ extern "C" {
 
 typedef void* lgcn_stream_t; /* a hipStream_t; NULL = the null stream */
 
-#define LGCN_ABI_VERSION 3
+#define LGCN_ABI_VERSION 4
 
 #define LGCN_OK 0
 #define LGCN_E_ARG (-1)         /* bad size / null pointer / unsupported argument */
@@ -306,6 +306,9 @@ int lgcn_bpr_fused_cols(const float* f_lo, const float* f_hi, int64_t f_split, c
  * (LGCN_LOSS_PARTS blocks over contiguous shares, one block over the shares): a fixed association
  * either way, so the loss is deterministic. */
 #define LGCN_LOSS_PARTS 256
+/* batches below this many triplets sum their loss in one block (lgcn_bpr_loss without partial
+ * scratch's second stage) — the sizes lgcn_range_scatter_add_loss can fold into its launch */
+#define LGCN_LOSS_FUSED_MAX_B 16384
 int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* loss, float* partial,
                   lgcn_stream_t stream);
 int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C, int64_t N, int32_t d,
@@ -334,6 +337,16 @@ int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_
                            const float* C2, const float* reg_w_lo, const float* reg_w_hi, int64_t reg_w_split,
                            float reg_coeff, int64_t reg_B, float* c2buf, uint8_t* c2flag, int32_t* overflow,
                            const uint8_t* store_unless, lgcn_stream_t stream);
+/* lgcn_range_scatter_add plus, as one extra workgroup of the same launch, lgcn_bpr_loss's
+ * single-block sum (the same block size, so the same association: bitwise its result) of
+ * terms[0 .. 2 loss_B) into loss[0] (ABI 4; 1 <= loss_B < LGCN_LOSS_FUSED_MAX_B, B >= 1, nrows >= 1).
+ * The step's loss launch folded into a launch it needs anyway (one launch fewer per small step). */
+int lgcn_range_scatter_add_loss(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
+                                int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
+                                const float* C2, const float* reg_w_lo, const float* reg_w_hi, int64_t reg_w_split,
+                                float reg_coeff, int64_t reg_B, float* c2buf, uint8_t* c2flag, int32_t* overflow,
+                                const uint8_t* store_unless, const float* terms, int64_t loss_B, int32_t loss_d,
+                                float loss_coeff, float* loss, lgcn_stream_t stream);
 /* The same per-row work as lgcn_range_scatter_add (flags, b-order sums, parked C2 sums, store or
  * add) for LARGE B, where every range-scatter workgroup streaming all B keys would cost O(B^2):
  * the keys arrive grouped by row in b order as rowptr[nrows+1] / perm[B] (= b) from

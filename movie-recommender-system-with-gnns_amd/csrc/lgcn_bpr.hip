@@ -203,10 +203,12 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
 constexpr int kLossBlock = 1024;
 constexpr int kLossPartBlock = 256;
 
-// Sums of t[0..n) and t[stride..stride+n) by one block (each thread its strided terms in index
-// order, loads issued 8 at a time, then the fixed wave/LDS tree), into the loss of B triplets.
-__global__ __launch_bounds__(kLossBlock) void k_bpr_loss(const float* __restrict__ t, int64_t n, int64_t stride,
-                                                         int64_t B, int32_t d, float coeff, float* __restrict__ loss) {
+// Sums of t[0..n) and t[stride..stride+n) by one block of kLossBlock threads (each thread its
+// strided terms in index order, loads issued 8 at a time, then the fixed wave/LDS tree), into the
+// loss of B triplets. Run as its own launch (k_bpr_loss) or as the extra workgroup of the range
+// scatter (k_range_scatter has the same block size): the same association either way.
+__device__ __forceinline__ void bpr_loss_block(const float* __restrict__ t, int64_t n, int64_t stride, int64_t B,
+                                               int32_t d, float coeff, float* __restrict__ loss) {
     __shared__ float r0[kLossBlock / 64], r1[kLossBlock / 64];
     float s0 = 0.f, s1 = 0.f;
     constexpr int kU = 8;
@@ -248,6 +250,20 @@ __global__ __launch_bounds__(kLossBlock) void k_bpr_loss(const float* __restrict
         loss[0] = -((a / bf) / 10.0f) + coeff * (c / (bf * static_cast<float>(d)));
     }
 }
+
+__global__ __launch_bounds__(kLossBlock) void k_bpr_loss(const float* __restrict__ t, int64_t n, int64_t stride,
+                                                         int64_t B, int32_t d, float coeff, float* __restrict__ loss) {
+    bpr_loss_block(t, n, stride, B, d, coeff, loss);
+}
+
+// the single-block loss sum as an extra workgroup of the range scatter (lgcn_range_scatter_add_loss)
+struct LossArgs {
+    const float* terms;
+    int64_t B;
+    int32_t d;
+    float coeff;
+    float* loss;
+};
 
 // First stage of the two-stage sum: block p sums its contiguous share of each term array (threads
 // strided in index order, then the fixed wave/LDS tree) into part[p] and part[P + p].
@@ -359,7 +375,12 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                                                             RegSrc reg,
                                                             float* __restrict__ c2buf, uint8_t* __restrict__ c2flag,
                                                             int* __restrict__ overflow,
-                                                            const uint8_t* __restrict__ store_unless) {
+                                                            const uint8_t* __restrict__ store_unless, LossArgs la) {
+    static_assert(kRSBlock == kLossBlock, "the loss workgroup needs the loss block's size (its association)");
+    if (la.loss != nullptr && blockIdx.x == gridDim.x - 1) {
+        bpr_loss_block(la.terms, la.B, la.B, la.B, la.d, la.coeff, la.loss);
+        return;
+    }
     constexpr int GPB = kRSBlock / LPR;
     const bool second = C2 != nullptr || reg.w_lo != nullptr;  // a second (parked) sum per row
     __shared__ int lkey[kRangeCap];
@@ -608,7 +629,7 @@ __global__ __launch_bounds__(kBlock) void k_flagged_rows_add(const int64_t* __re
 template <int LPR, int NV>
 int launch_rs(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C, int32_t d, float* lo,
               float* hi, int64_t split, float mul, float div, const float* C2, RegSrc reg, float* c2buf,
-              uint8_t* c2flag, int* overflow, const uint8_t* store_unless, hipStream_t s) {
+              uint8_t* c2flag, int* overflow, const uint8_t* store_unless, const LossArgs& la, hipStream_t s) {
     // every workgroup streams all B keys once; enough workgroups that each keeps ~<= 256 entries
     // on average (the list holds kRangeCap), at least 256 (one per CU)
     int64_t wgs = B / 256 + 1;
@@ -616,10 +637,11 @@ int launch_rs(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset,
     if (wgs > 65535) wgs = 65535;
     if (wgs > nrows) wgs = nrows > 0 ? nrows : 1;
     const int64_t span = (nrows + wgs - 1) / wgs;
-    const int64_t grid = (nrows + span - 1) / span;
+    const int64_t grid = (nrows + span - 1) / span + (la.loss != nullptr ? 1 : 0);  // + the loss workgroup
     k_range_scatter<LPR, NV><<<dim3(static_cast<unsigned>(grid)), kRSBlock, 0, s>>>(keys, B, nrows, span, key_offset, C, d,
                                                                                  lo, hi, split, mul, div, C2, reg,
-                                                                                 c2buf, c2flag, overflow, store_unless);
+                                                                                 c2buf, c2flag, overflow, store_unless,
+                                                                                 la);
     return check_launch("k_range_scatter");
 }
 
@@ -720,6 +742,41 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 }  // namespace
 
+namespace {
+
+int range_scatter(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C, int32_t d,
+                  float* out_lo, float* out_hi, int64_t split, float mul, float div, const float* C2,
+                  const float* reg_w_lo, const float* reg_w_hi, int64_t reg_w_split, float reg_coeff, int64_t reg_B,
+                  float* c2buf, uint8_t* c2flag, int32_t* overflow, const uint8_t* store_unless, const LossArgs& la,
+                  lgcn_stream_t stream) {
+    const bool second = C2 != nullptr || reg_w_lo != nullptr;
+    if (B < 0 || d <= 0 || nrows < 0 || (B > 0 && (!keys || !C || !out_lo)) || (second && (!c2buf || !c2flag)) ||
+        (C2 && reg_w_lo))
+        return fail(LGCN_E_ARG, "lgcn_range_scatter_add: bad args");
+    if (B == 0) return LGCN_OK;
+    if (nrows == 0)  // no key is in range: nothing to add, every flag 0
+        return second ? check_hip(hipMemsetAsync(c2flag, 0, static_cast<size_t>(B), as_stream(stream)), "memset c2flag")
+                      : LGCN_OK;
+    if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C2 && !al16(C2)) ||
+        (second && !al16(c2buf)) || (reg_w_lo && (!al16(reg_w_lo) || (reg_w_hi && !al16(reg_w_hi)))))
+        return fail(LGCN_E_UNSUPPORTED, "lgcn_range_scatter_add: needs d %% 4 == 0 and aligned rows");
+    hipStream_t s = as_stream(stream);
+    const RegSrc reg{reg_w_lo, reg_w_hi, reg_w_split, reg_coeff, reg_B};
+#define LGCN_RS(L, V) launch_rs<L, V>(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg, c2buf, c2flag, overflow, store_unless, la, s)
+    switch (d) {
+        case 8: return LGCN_RS(2, 1);
+        case 16: return LGCN_RS(4, 1);
+        case 32: return LGCN_RS(8, 1);
+        case 64: return LGCN_RS(16, 1);
+        case 128: return LGCN_RS(32, 1);
+        case 256: return LGCN_RS(64, 1);
+        case 512: return LGCN_RS(64, 2);
+        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_range_scatter_add: d=%d", d);
+    }
+#undef LGCN_RS
+}
+}  // namespace
+
 extern "C" {
 
 int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split, const float* w_lo, const float* w_hi,
@@ -755,37 +812,31 @@ int lgcn_bpr_fused_cols(const float* f_lo, const float* f_hi, int64_t f_split, c
     return bpr_dispatch(a, phase, as_stream(stream));
 }
 
+
 int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
                            int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
                            const float* C2, const float* reg_w_lo, const float* reg_w_hi, int64_t reg_w_split,
                            float reg_coeff, int64_t reg_B, float* c2buf, uint8_t* c2flag, int32_t* overflow,
                            const uint8_t* store_unless, lgcn_stream_t stream) {
-    const bool second = C2 != nullptr || reg_w_lo != nullptr;
-    if (B < 0 || d <= 0 || nrows < 0 || (B > 0 && (!keys || !C || !out_lo)) || (second && (!c2buf || !c2flag)) ||
-        (C2 && reg_w_lo))
-        return fail(LGCN_E_ARG, "lgcn_range_scatter_add: bad args");
-    if (B == 0) return LGCN_OK;
-    if (nrows == 0)  // no key is in range: nothing to add, every flag 0
-        return second ? check_hip(hipMemsetAsync(c2flag, 0, static_cast<size_t>(B), as_stream(stream)), "memset c2flag")
-                      : LGCN_OK;
-    if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C2 && !al16(C2)) ||
-        (second && !al16(c2buf)) || (reg_w_lo && (!al16(reg_w_lo) || (reg_w_hi && !al16(reg_w_hi)))))
-        return fail(LGCN_E_UNSUPPORTED, "lgcn_range_scatter_add: needs d %% 4 == 0 and aligned rows");
-    hipStream_t s = as_stream(stream);
-    const RegSrc reg{reg_w_lo, reg_w_hi, reg_w_split, reg_coeff, reg_B};
-#define LGCN_RS(L, V) launch_rs<L, V>(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg, c2buf, c2flag, overflow, store_unless, s)
-    switch (d) {
-        case 8: return LGCN_RS(2, 1);
-        case 16: return LGCN_RS(4, 1);
-        case 32: return LGCN_RS(8, 1);
-        case 64: return LGCN_RS(16, 1);
-        case 128: return LGCN_RS(32, 1);
-        case 256: return LGCN_RS(64, 1);
-        case 512: return LGCN_RS(64, 2);
-        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_range_scatter_add: d=%d", d);
-    }
-#undef LGCN_RS
+    return range_scatter(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg_w_lo, reg_w_hi,
+                         reg_w_split, reg_coeff, reg_B, c2buf, c2flag, overflow, store_unless,
+                         LossArgs{nullptr, 0, 0, 0.f, nullptr}, stream);
 }
+
+int lgcn_range_scatter_add_loss(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
+                                int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
+                                const float* C2, const float* reg_w_lo, const float* reg_w_hi, int64_t reg_w_split,
+                                float reg_coeff, int64_t reg_B, float* c2buf, uint8_t* c2flag, int32_t* overflow,
+                                const uint8_t* store_unless, const float* terms, int64_t loss_B, int32_t loss_d,
+                                float loss_coeff, float* loss, lgcn_stream_t stream) {
+    if (!terms || !loss || loss_B < 1 || loss_d <= 0 || loss_B >= LGCN_LOSS_FUSED_MAX_B || B <= 0 || nrows <= 0)
+        return fail(LGCN_E_ARG, "lgcn_range_scatter_add_loss: bad loss args (B=%lld; the single-block sum needs "
+                    "1 <= B < %d, and a scatter with work)", (long long)loss_B, LGCN_LOSS_FUSED_MAX_B);
+    return range_scatter(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg_w_lo, reg_w_hi,
+                         reg_w_split, reg_coeff, reg_B, c2buf, c2flag, overflow, store_unless,
+                         LossArgs{terms, loss_B, loss_d, loss_coeff, loss}, stream);
+}
+
 
 int lgcn_sorted_scatter_add(const int64_t* rowptr, const int32_t* perm, int64_t nrows, int64_t key_offset,
                             const float* C, int32_t d, float* out_lo, float* out_hi, int64_t split, float mul,
@@ -887,7 +938,9 @@ int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* 
     hipStream_t s = as_stream(stream);
     // large batches: LGCN_LOSS_PARTS blocks sum contiguous shares, one block sums the shares
     // (a single block over 2B terms is latency-bound: 26 us at B = 180k)
-    if (partial != nullptr && B >= 16 * int64_t(LGCN_LOSS_PARTS) * kLossPartBlock / 64) {
+    static_assert(LGCN_LOSS_FUSED_MAX_B == 16 * LGCN_LOSS_PARTS * kLossPartBlock / 64,
+                  "the fused loss covers exactly the single-block sizes");
+    if (partial != nullptr && B >= LGCN_LOSS_FUSED_MAX_B) {
         k_bpr_loss_part<<<LGCN_LOSS_PARTS, kLossPartBlock, 0, s>>>(terms, B, partial);
         if (int rc = check_launch("k_bpr_loss_part")) return rc;
         k_bpr_loss<<<1, kLossBlock, 0, s>>>(partial, LGCN_LOSS_PARTS, LGCN_LOSS_PARTS, B, d, coeff, loss);

@@ -25,11 +25,12 @@ E_ARG, E_WORKSPACE, E_UNSUPPORTED = -1, -2, -3  # include/lgcn.h LGCN_E_*
 
 ITEM_BYTES = 16   # lgcn_item_t {int64 beg; int32 len; int32 dst}
 SPLIT_BYTES = 16  # lgcn_split_t {int32 row, pbeg, pcnt, pad}
-ABI_VERSION = 3  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
+ABI_VERSION = 4  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
 
 _lib = None
 
 LOSS_PARTS = 256  # include/lgcn.h LGCN_LOSS_PARTS
+LOSS_FUSED_MAX_B = 16384  # include/lgcn.h LGCN_LOSS_FUSED_MAX_B
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
 _i32 = ctypes.c_int32
@@ -77,6 +78,9 @@ _SIGS = {
     "lgcn_segment_rows": ([_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _i32, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_range_scatter_add": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _i64,
                                 _f32, _i64, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
+    "lgcn_range_scatter_add_loss": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp,
+                                     _i64, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _vp, _vp],
+                                    ctypes.c_int),
     "lgcn_sorted_scatter_add": ([_vp, _vp, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _i64,
                                  _f32, _i64, _vp, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_grouped_reg_add": ([_vp, _i64, _i64, _vp, _vp, _i64, _i32, _f32, _i64, _vp, _vp, _i64, _vp], ctypes.c_int),

@@ -244,20 +244,34 @@ def sorted_scatter_min_b() -> int:
     return int(os.environ.get("LGCN_SORTED_SCATTER_MIN_B", 49152))
 
 
+def loss_fused(st, I: int, cols=None) -> bool:
+    """Whether the step's loss sum rides in the range scatter's launch (lgcn_range_scatter_add_loss:
+    one extra workgroup, the same single-block sum as lgcn_bpr_loss) instead of its own launch:
+    the range-scatter path, a batch small enough for the single-block sum, full-width rows."""
+    return cols is None and st.neg_rowptr is None and I > 0 and 1 <= st.B < _ffi.LOSS_FUSED_MAX_B
+
+
 def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: float, store_unless, stream,
-                      uw, iw, coeff: float) -> None:
+                      uw, iw, coeff: float, loss=None) -> None:
     """dF rows of the step's negatives into the gradient tables and the first-occurrence flags
     (st.c2flag); the range scatter also parks each row's reg-rows sum (formed from the layer-0
-    rows uw / iw) in its first-occurrence slot for add_negative_reg_rows after the backward."""
+    rows uw / iw) in its first-occurrence slot for add_negative_reg_rows after the backward.
+    loss = (terms, d, coeff, out): the step's loss sum in the same launch (loss_fused)."""
     B = st.B
     C = st.cf[2 * B:]
     reg = (None, uw.data_ptr(), iw.data_ptr(), U, coeff, B)
     if st.neg_rowptr is None:
-        _ffi.check(lib.lgcn_range_scatter_add(st.neg.data_ptr(), B, I, U, C.data_ptr(), d, gu.data_ptr(), gi.data_ptr(),
-                                              U, mul, div, *reg, st.c2buf.data_ptr(), st.c2flag.data_ptr(),
-                                              st.overflow.data_ptr(), _ffi.ptr(store_unless), stream),
-                   "lgcn_range_scatter_add")
+        common = (st.neg.data_ptr(), B, I, U, C.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U, mul, div, *reg,
+                  st.c2buf.data_ptr(), st.c2flag.data_ptr(), st.overflow.data_ptr(), _ffi.ptr(store_unless))
+        if loss is not None:
+            terms, ld, lcoeff, out = loss
+            _ffi.check(lib.lgcn_range_scatter_add_loss(*common, terms.data_ptr(), B, ld, lcoeff, out.data_ptr(),
+                                                       stream), "lgcn_range_scatter_add_loss")
+        else:
+            _ffi.check(lib.lgcn_range_scatter_add(*common, stream), "lgcn_range_scatter_add")
         return
+    if loss is not None:
+        raise ValueError("scatter_negatives: the fused loss needs the range-scatter path")
     if st.neg_grouping == "radix":
         _ffi.check(lib.lgcn_csr_build(st.neg.data_ptr(), st.neg.data_ptr(), B, I, st.neg_rowptr.data_ptr(),
                                       st.neg_col.data_ptr(), st.neg_perm.data_ptr(), st.neg_err.data_ptr(),
@@ -405,9 +419,11 @@ class FusedTrainStep:
                                           st.plan.touched.data_ptr(), div, mul,
                                           self.coeff, st.cf.data_ptr(), _ffi.ptr(st.cw), st.terms.data_ptr(),
                                           stream), "lgcn_bpr_fused")
-            _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(),
-                                         st.loss_part.data_ptr(), stream),
-                       "lgcn_bpr_loss")
+            fused = st.small and loss_fused(st, I)
+            if not fused:
+                _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(),
+                                             st.loss_part.data_ptr(), stream),
+                           "lgcn_bpr_loss")
             gu = torch.empty((U, d), dtype=torch.float32, device=dev)
             gi = torch.empty((I, d), dtype=torch.float32, device=dev)
             grads = (gu, gi, U)
@@ -418,7 +434,8 @@ class FusedTrainStep:
                 spmm(st.fixed_dense, N, d, (st.cf, None, big), None, grads, None, _ffi.EPI_SCALE, div, mul,
                      stream=stream)
                 # negatives: dF rows into g now, their reg rows parked (per row, first-occurrence slot)
-                scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, None, stream, uw, iw, self.coeff)
+                scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, None, stream, uw, iw, self.coeff,
+                                  (st.terms, d, self.coeff, st.loss) if fused else None)
                 propagate_backward_seeded(gu, gi, st.plan, K)
                 add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, self.coeff, stream)
                 add_negative_reg_rows(lib, st, gu, gi, U, d, uw, iw, self.coeff, stream)
@@ -449,8 +466,9 @@ class FusedTrainStep:
                                           st.plan.touched.data_ptr(), div, mul,
                                           self.coeff, st.cf.data_ptr(), _ffi.ptr(st.cw), st.terms.data_ptr(),
                                           stream), "lgcn_bpr_fused")
-            _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(),
-                                         st.loss_part.data_ptr(), stream), "lgcn_bpr_loss")
+            if not loss_fused(st, N - U):  # else the range scatter's launch sums it (_step_lazy)
+                _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(),
+                                             st.loss_part.data_ptr(), stream), "lgcn_bpr_loss")
             return self.coeff
         if getattr(st, "sums", None) is None:
             st.sums = torch.empty(max(1, 6 * B), dtype=torch.float32, device=uw.device)
@@ -501,7 +519,8 @@ class FusedTrainStep:
             spmm(st.fixed_touched, N, d, (st.cf, None, big), None, grads, None, _ffi.EPI_SCALE, div, mul,
                  stream=stream)
             # ... the negatives' rows added (stored where the row is outside the touched set)
-            scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream, uw, iw, reg_coeff)
+            scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream, uw, iw, reg_coeff,
+                              (st.terms, d, self.coeff, st.loss) if loss_fused(st, I, self.cols) else None)
             propagate_backward_seeded(gu, gi, st.plan, K)
             add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, reg_coeff, stream)
             add_negative_reg_rows(lib, st, gu, gi, U, d, uw, iw, reg_coeff, stream)

@@ -347,3 +347,53 @@ def test_sorted_no_parking_plus_grouped_reg_equals_parked(gpu, B, nrows, d):
         res.append((out.cpu(), flag.cpu()))
     assert torch.equal(res[0][1], res[1][1])
     assert torch.equal(res[0][0], res[1][0])
+
+
+@pytest.mark.parametrize("B,nrows,d", [(1, 7, 64), (1000, 500, 64), (10000, 59047, 128), (16383, 5000, 32)])
+def test_range_scatter_with_loss_workgroup_bitwise(gpu, B, nrows, d):
+    """lgcn_range_scatter_add_loss (the step's loss sum as one extra workgroup of the scatter's
+    launch) writes the same scatter results and flags as lgcn_range_scatter_add and the same loss,
+    bit for bit, as lgcn_bpr_loss's own single-block launch."""
+    from lgcn_amd import _ffi
+
+    lib = _ffi.load()
+    rng = np.random.default_rng(B + d)
+    keys = torch.from_numpy(rng.integers(0, nrows, B).astype(np.int64)).to(gpu)
+    C = torch.from_numpy(rng.standard_normal((B, d)).astype(np.float32)).to(gpu)
+    C2 = torch.from_numpy(rng.standard_normal((B, d)).astype(np.float32)).to(gpu)
+    terms = torch.from_numpy((rng.standard_normal(2 * B) * 3).astype(np.float32)).to(gpu)
+    out0 = torch.from_numpy(rng.standard_normal((nrows, d)).astype(np.float32)).to(gpu)
+    s = _ffi.stream_of(gpu)
+    res = []
+    for fused in (False, True):
+        out = out0.clone()
+        buf = torch.empty((B, d), dtype=torch.float32, device=gpu)
+        flag = torch.empty(B, dtype=torch.uint8, device=gpu)
+        ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+        loss = torch.full((1,), float("nan"), dtype=torch.float32, device=gpu)
+        common = (keys.data_ptr(), B, nrows, 0, C.data_ptr(), d, out.data_ptr(), None, nrows, 0.25, 4.0,
+                  C2.data_ptr(), None, None, 0, 0.0, 0, buf.data_ptr(), flag.data_ptr(), ovf.data_ptr(), None)
+        if fused:
+            _ffi.check(lib.lgcn_range_scatter_add_loss(*common, terms.data_ptr(), B, d, 1e-4, loss.data_ptr(), s),
+                       "lgcn_range_scatter_add_loss")
+        else:
+            _ffi.check(lib.lgcn_range_scatter_add(*common, s), "lgcn_range_scatter_add")
+            _ffi.check(lib.lgcn_bpr_loss(terms.data_ptr(), B, d, 1e-4, loss.data_ptr(), None, s), "lgcn_bpr_loss")
+        res.append((out.cpu().numpy(), buf.cpu().numpy(), flag.cpu().numpy(), float(loss.item()), int(ovf.item())))
+    (o0, b0, f0, l0, v0), (o1, b1, f1, l1, v1) = res
+    assert np.array_equal(o0, o1) and np.array_equal(f0, f1) and v0 == v1 == 0
+    assert np.array_equal(b0[f0 == 1], b1[f1 == 1])  # parked sums (first-occurrence slots)
+    assert np.float32(l0).tobytes() == np.float32(l1).tobytes() and np.isfinite(l1)
+
+
+def test_range_scatter_loss_rejects_two_stage_sizes(gpu):
+    """The fused loss covers only the single-block sums: B >= LGCN_LOSS_FUSED_MAX_B is refused."""
+    from lgcn_amd import _ffi
+
+    lib = _ffi.load()
+    B = _ffi.LOSS_FUSED_MAX_B
+    z = torch.zeros(1, dtype=torch.float32, device=gpu)
+    rc = lib.lgcn_range_scatter_add_loss(z.data_ptr(), B, 10, 0, z.data_ptr(), 64, z.data_ptr(), None, 10, 1.0, 1.0,
+                                         None, None, None, 0, 0.0, 0, None, None, None, None, z.data_ptr(), B, 64,
+                                         0.0, z.data_ptr(), _ffi.stream_of(gpu))
+    assert rc == _ffi.E_ARG
