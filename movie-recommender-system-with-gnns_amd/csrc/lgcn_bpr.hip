@@ -740,10 +740,7 @@ int launch_seg(const int64_t* rowptr, const int32_t* perm, const float* C, int64
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-}  // namespace
-
-namespace {
-
+// lgcn_range_scatter_add(_loss): argument checks, then the width dispatch
 int range_scatter(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C, int32_t d,
                   float* out_lo, float* out_hi, int64_t split, float mul, float div, const float* C2,
                   const float* reg_w_lo, const float* reg_w_hi, int64_t reg_w_split, float reg_coeff, int64_t reg_B,
@@ -811,7 +808,6 @@ int lgcn_bpr_fused_cols(const float* f_lo, const float* f_hi, int64_t f_split, c
               sums, d_full};
     return bpr_dispatch(a, phase, as_stream(stream));
 }
-
 
 int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
                            int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
