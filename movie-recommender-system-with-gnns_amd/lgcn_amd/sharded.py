@@ -375,6 +375,7 @@ class BlockExchange:
         if len(self.members) != shards.W:
             raise ValueError(f"{len(self.members)} exchange members for {shards.W} row groups")
         self.nccl = device_collectives(group)
+        self.rccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
         self.stream = None
         self.bytes = 0  # received per rank, over the run
 
@@ -401,6 +402,10 @@ class BlockExchange:
             with torch.cuda.stream(self.stream):
                 self.stream.wait_event(ready)
                 if self.mode == "p2p":
+                    if not self.rccl:
+                        # gloo's send/recv move a device tensor's bytes from the host, outside
+                        # every stream: the block must be final and its old readers done first
+                        torch.cuda.synchronize(buf.device)
                     for req in self.dist.batch_isend_irecv(self._p2p_ops(out, mine, c)):
                         req.wait()
                 else:
