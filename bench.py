@@ -170,11 +170,12 @@ def child_envs(n: int, port: int, base=None) -> list:
     return envs
 
 
-def launch_ranks(n: int, argv: list, script=None) -> int:
+def launch_ranks(n: int, argv: list, script=None, relayed: list | None = None) -> int:
     """`python bench.py --gpus N` outside torchrun: start N rank processes of this script (one per
     GPU, LOCAL_RANK = GPU index) and wait for them. This process touches no GPU (it imports neither
     torch nor lgcn_amd). Rank 0's stdout (the JSON line) is relayed; if any rank fails the others
-    are stopped and its exit code is returned. script: the rank program (tests; default this file)."""
+    are stopped and its exit code is returned. script: the rank program (tests; default this file);
+    relayed: a list that receives the relayed JSON lines."""
     import signal
     import subprocess
 
@@ -214,7 +215,7 @@ def launch_ranks(n: int, argv: list, script=None) -> int:
         signal.signal(sig, stop_all)
     import threading
 
-    out = []
+    out = relayed if relayed is not None else []
 
     def relay():
         # the JSON line to stdout; anything else a library prints there (gloo, RCCL) to stderr
@@ -258,6 +259,22 @@ def launch_ranks(n: int, argv: list, script=None) -> int:
     if rc == 0 and not out:
         log("launch: rank 0 printed nothing")
         rc = 1
+    return rc
+
+
+def launch_with_fallback(args, launch=None) -> int:
+    """launch_ranks, and once more without the peer-send grid candidates (LGCN_GRID_NO_P2P=1) when
+    a C2 grid run ended with no result: those candidates are timed last and are the one exchange
+    outside RCCL's plain collectives, so a rank stuck in one ends the run at the process-group
+    timeout before a grid is picked — the second launch then times the plain candidates only."""
+    launch = launch or launch_ranks
+    out = []
+    rc = launch(args.gpus, sys.argv[1:], relayed=out)
+    if (rc != 0 and not out and args.gpus >= 3 and args.workload == "propagate" and args.config == "c2"
+            and not args.shard and os.environ.get("LGCN_GRID_NO_P2P") != "1"):
+        log(f"launch: no result (exit {rc}); launching again without the peer-send grid candidates")
+        os.environ["LGCN_GRID_NO_P2P"] = "1"
+        rc = launch(args.gpus, sys.argv[1:], relayed=out)
     return rc
 
 
@@ -401,7 +418,7 @@ def main():
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # plain `python bench.py --gpus N`: become the launcher of N ranks (torchrun sets WORLD_SIZE)
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(launch_with_fallback(args))
     if args.workload == "train":
         return run_train(args)
 
@@ -520,7 +537,10 @@ def main():
             # A candidate that raises on any rank is skipped on every rank (the ranks agree through
             # one all_reduce of [ms, failed] per candidate), so one bad grid cannot end the run.
             st, best, grid_trials = None, None, {}
-            for R, F, mode in grid_candidates(world, d_full):
+            p2p = os.environ.get("LGCN_GRID_NO_P2P") != "1"  # launch_with_fallback's second launch
+            if not p2p and any(m == "p2p" for _, _, m in grid_candidates(world, d_full)):
+                grid_trials["p2p candidates"] = "skipped (LGCN_GRID_NO_P2P=1)"
+            for R, F, mode in grid_candidates(world, d_full, p2p=p2p):
                 name = f"{R}x{F}" + (f"/{mode}" if mode else "")
                 cand, ms, failed = None, 0.0, 0.0
                 try:

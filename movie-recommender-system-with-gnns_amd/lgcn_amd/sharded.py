@@ -168,7 +168,8 @@ def grid_shape(world: int, d: int) -> tuple[int, int]:
     return world, 1
 
 
-def grid_candidates(world: int, d: int, bipartite: bool = True) -> list[tuple[int, int, str | None]]:
+def grid_candidates(world: int, d: int, bipartite: bool = True,
+                    p2p: bool = True) -> list[tuple[int, int, str | None]]:
     """(R, F, exchange mode) grids bench.py times before it picks one for a world of ranks (mode
     "reduce" — users sharded, item rows all-reduced — for every R > 1 of a bipartite graph): every
     column split F | world with d / F a multiple of 4 and >= 8; the rows-only grid (F = 1) when no
@@ -176,7 +177,7 @@ def grid_candidates(world: int, d: int, bipartite: bool = True) -> list[tuple[in
     at once, so its bytes per xGMI link match the column-split grids' (C2 at N = 8: ~14 MB per link
     per step for 8 x 1, 4 x 2 and 2 x 4) at the least compute per rank; both exchange modes where a
     row group has three or more ranks (an all_gather and direct peer sends differ there), none with
-    R = 1."""
+    R = 1. p2p=False: without the peer-send candidates."""
     out = []
     for F in range(world, 0, -1):
         if world % F or d % F or (d // F) % 4 or d // F < 8:
@@ -193,7 +194,7 @@ def grid_candidates(world: int, d: int, bipartite: bool = True) -> list[tuple[in
     # the peer-send candidates last: batch_isend_irecv is the one exchange outside RCCL's plain
     # collectives, so the log holds every plain candidate's time before them (a candidate that
     # raises is skipped either way; one that hangs ends the run at the process-group timeout)
-    return [c for c in out if c[2] != "p2p"] + [c for c in out if c[2] == "p2p"]
+    return [c for c in out if c[2] != "p2p"] + ([c for c in out if c[2] == "p2p"] if p2p else [])
 
 
 @dataclasses.dataclass

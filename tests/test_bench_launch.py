@@ -132,3 +132,38 @@ def test_launcher_stops_its_ranks_when_stopped(tmp_path):
     for f in pids.iterdir():
         with pytest.raises(ProcessLookupError):
             os.kill(int(f.name), 0)
+
+
+def _args(**kw):
+    import argparse
+
+    base = dict(gpus=8, workload="propagate", config="c2", shard=None)
+    base.update(kw)
+    return argparse.Namespace(**base)
+
+
+@pytest.mark.parametrize("first_rc,first_out,kw,relaunched", [
+    (1, [], {}, True),                          # no result: once more without the peer-send grids
+    (1, [b"{}\n"], {}, False),                  # a result was relayed: never a second line
+    (0, [b"{}\n"], {}, False),
+    (1, [], {"gpus": 2}, False),                # no p2p candidate below 3 ranks per row group
+    (1, [], {"workload": "train"}, False),
+    (1, [], {"config": "c5"}, False),
+    (1, [], {"shard": "4x2"}, False),
+])
+def test_launch_fallback_without_p2p(monkeypatch, first_rc, first_out, kw, relaunched):
+    b = _bench()
+    monkeypatch.delenv("LGCN_GRID_NO_P2P", raising=False)
+    calls = []
+
+    def fake_launch(n, argv, relayed):
+        calls.append(os.environ.get("LGCN_GRID_NO_P2P"))
+        if len(calls) == 1:
+            relayed.extend(first_out)
+            return first_rc
+        relayed.append(b"{}\n")
+        return 0
+
+    rc = b.launch_with_fallback(_args(**kw), launch=fake_launch)
+    assert calls == ([None, "1"] if relaunched else [None])
+    assert rc == (0 if relaunched else first_rc)

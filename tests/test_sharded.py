@@ -343,3 +343,12 @@ def test_reduce_mode_matches_oracle(tmp_path, kind, world, K, F):
         log = list(np.load(tmp_path / "log0.npy"))
         expect = ["partial", "users"] + ["partial", "items", "users"] * (K - 1) + ["items"]
         assert log == expect, log
+
+
+def test_grid_candidates_without_p2p():
+    from lgcn_amd.sharded import grid_candidates
+
+    for world in (3, 4, 8):
+        full = grid_candidates(world, 64)
+        assert grid_candidates(world, 64, p2p=False) == [c for c in full if c[2] != "p2p"]
+        assert any(c[2] == "p2p" for c in full)
