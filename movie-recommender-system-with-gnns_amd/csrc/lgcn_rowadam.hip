@@ -58,6 +58,10 @@ __device__ __forceinline__ T* trow(T* lo, T* hi, int64_t split, int64_t r, int64
     return r < split ? lo + r * d : hi + (r - split) * d;
 }
 
+#ifndef LGCN_ADAM_EARLY_LAST
+#define LGCN_ADAM_EARLY_LAST 1
+#endif
+
 #ifndef LGCN_ADAM_MARKSTEIN
 #define LGCN_ADAM_MARKSTEIN 1
 #endif
@@ -140,12 +144,20 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
     const bool upd = mode == 1 || mode == 3;
     const int64_t t = step[0] - (mode == 3 ? 1 : 0);
     int64_t row;
+    int32_t last_row;
     if (mode == 2) {
         if (i >= n_rows) return;
         row = i;
+        last_row = last[row];
     } else {
         if (i >= L.n_a + L.n_b) return;
-        if (!list_row(L, i, row)) return;
+        const bool listed = list_row(L, i, row);
+#if LGCN_ADAM_EARLY_LAST
+        // issued beside the list filters and the claim instead of after them: only this row's
+        // winner ever writes last[row] (its lane 0, at the end), so the value is the same
+        last_row = last[row];
+#endif
+        if (!listed) return;
         if (mode == 0) {
             // duplicates in the catch-up list: the first claimer of this step's stamp does the work
             int won = 0;
@@ -154,7 +166,10 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
             if (!won) return;
         }
     }
-    const int64_t from = int64_t(last[row]) + 1;
+#if !LGCN_ADAM_EARLY_LAST
+    if (mode != 2) last_row = last[row];
+#endif
+    const int64_t from = int64_t(last_row) + 1;
     const int64_t upto = t;  // zero-gradient replays through step t
     // a catch-up (or flush) of a row that is already current touches nothing (on the planted
     // graph ~95 % of a step's negative rows were updated the step before: no p/m/v traffic)
