@@ -391,7 +391,7 @@ def main():
     ap.add_argument("--shard", default=None,
                     help="c2, N > 1: RxF grid (R row groups x F column groups, R*F = N); default: every "
                          "lgcn_amd.sharded.grid_candidates grid is timed for a few steps and the fastest runs")
-    ap.add_argument("--exchange-mode", choices=["allgather", "p2p", "reduce"], default="allgather",
+    ap.add_argument("--exchange-mode", choices=["allgather", "p2p", "reduce", "reduce-fused"], default="allgather",
                     help="c2 with --shard and R > 1: one all_gather per block, or sends to every peer")
     ap.add_argument("--workload", choices=["propagate", "train"], default="propagate",
                     help="propagate: C2 headline (default); train: C3/C4 Cluster-GCN training steps")
@@ -499,14 +499,16 @@ def main():
                             mode=None, step=lambda: lgcn_amd.propagate_forward(uw_c, iw_c, cplan, K))
             if (grid.R, grid.F) not in groups:  # collective: every rank creates the column groups
                 groups[(grid.R, grid.F)] = grid.exchange_group(dist)
-            if mode == "reduce":
-                # users sharded, item rows all-reduced per layer (lgcn_amd.sharded.ReducePlan)
+            if mode in ("reduce", "reduce-fused"):
+                # users sharded, item rows all-reduced per layer (lgcn_amd.sharded.ReducePlan);
+                # reduce-fused: a layer's two passes as one lgcn_spmm_pair launch (+ one combine)
                 ushards = UserShards.build(in_deg, U, grid.R)
                 rplan = ReducePlan(ei, ushards, grid.row_group, c1 - c0, chunk)
                 red = ItemReducer(grid.R, groups[(grid.R, grid.F)])
                 x0u, x0i = user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous()
+                fused = mode == "reduce-fused"
                 return dict(grid=grid, shards=ushards, splan=rplan, scheds=[rplan.users, rplan.partial], ex=red,
-                            mode=mode, step=lambda: propagate_forward_reduced(x0u, x0i, rplan, K, red))
+                            mode=mode, step=lambda: propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused))
             shards = RowShards.build(in_deg, U, grid.R)
             splan = ShardedPlan(ei, shards, grid.row_group, c1 - c0, chunk)
             x0p = shards.to_padded(user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous())
@@ -577,7 +579,7 @@ def main():
         if shards is None:
             log(f"[rank {rank}] grid {grid.R}x{grid.F}: all rows, columns [{c0}, {c1}) with the one-GPU plan at "
                 f"width {d}, {time.perf_counter() - t0:.2f} s")
-        elif st["mode"] == "reduce":
+        elif str(st["mode"]).startswith("reduce"):
             ua, ub_ = shards.users(g_r)
             log(f"[rank {rank}] grid {grid.R}x{grid.F} reduce: row group {g_r} (users {ub_ - ua} of {U}, all {I} "
                 f"items from {splan.n_sub} edges), columns [{c0}, {c1}), {time.perf_counter() - t0:.2f} s")
@@ -685,7 +687,7 @@ def main():
                                    f"partials are all-reduced within the column group once per layer "
                                    f"({args.dist_backend}, overlapped with the user pass and the next partial pass); "
                                    f"column groups exchange nothing; within 1e-5 per row of the 1-GPU result"
-                                   if sharded and st["mode"] == "reduce" else
+                                   if sharded and str(st["mode"]).startswith("reduce") else
                                    f"{grid.R} row groups x {grid.F} column groups over {world} GPUs: each rank "
                                    f"propagates {d} of {d_full} columns of one edge-balanced destination row range "
                                    f"(whole graph and whole column share of the table on every rank); " +
@@ -714,8 +716,8 @@ def main():
     if grid_trials is not None:
         result["config"]["grid_trials_ms_per_step"] = grid_trials
     if exchange is not None:
-        if st["mode"] == "reduce":
-            result["exchange"] = {"mode": "reduce", "all_reduces_per_step": K - 1, "reduce_scatters_per_step": 1,
+        if str(st["mode"]).startswith("reduce"):
+            result["exchange"] = {"mode": st["mode"], "all_reduces_per_step": K - 1, "reduce_scatters_per_step": 1,
                                   "MB_received_per_rank_per_step": exchange.bytes / args.steps / 1e6}
         else:
             result["exchange"] = {"mode": exchange.mode, "block_exchanges_per_step": 2 * (K - 1),

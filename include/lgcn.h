@@ -38,7 +38,7 @@ extern "C" {
 
 typedef void* lgcn_stream_t; /* a hipStream_t; NULL = the null stream */
 
-#define LGCN_ABI_VERSION 4
+#define LGCN_ABI_VERSION 5
 
 #define LGCN_OK 0
 #define LGCN_E_ARG (-1)         /* bad size / null pointer / unsupported argument */
@@ -258,6 +258,50 @@ int lgcn_spmm_blocksplit(const lgcn_item_t* items, int64_t n_items, const lgcn_s
                          float* y, float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
                          float div, float mul, lgcn_stream_t stream, const lgcn_item_t* chunks);
 
+/* Two independent plain passes of one width d over N-row tables, each described by the arguments
+ * lgcn_spmm takes (lgcn_pass_t below), issued together: what = 1 runs both item passes in ONE
+ * launch (workgroups of a first, then b's, each in its own longest-first order), what = 2 both
+ * combine passes in one launch, what = 3 both. Per row the result is bitwise what lgcn_spmm_items /
+ * lgcn_spmm_combine give for each pass alone; the two passes must not write what the other reads.
+ * The reduce-mode sharded forward (lgcn_amd/sharded.py) pairs a layer's user pass (users from the
+ * item table) with its item-partial pass (items from the rank's users): one launch gap and one
+ * drain per pair instead of two. Vector widths only (d in {4, 8, ..., 1024}, 16-byte aligned rows).
+ * Replaces, like lgcn_spmm, LGConv.forward at reference models/light_gcn.py:33 (ABI 5). */
+typedef struct {
+    const lgcn_item_t* items;
+    int64_t n_items;
+    const lgcn_split_t* splits;
+    int64_t n_splits;
+    const int32_t* col;
+    const float* val;
+    const float* x_lo;
+    const float* x_hi;
+    int64_t x_split;
+    const float* e_lo;
+    const float* e_hi;
+    int64_t e_split;
+    float* y;
+    float* acc_lo;
+    float* acc_hi;
+    int64_t acc_split;
+    float* partial;
+    int32_t mode;
+    float div;
+    float mul;
+} lgcn_pass_t;
+int lgcn_spmm_pair(const lgcn_pass_t* a, const lgcn_pass_t* b, int64_t N, int32_t d, int32_t what,
+                   lgcn_stream_t stream);
+
+/* The layer-stack mean of rows whose layer outputs were kept instead of accumulated (ABI 5):
+ * out[r] = ((((e[r] + y_0[r]) + y_1[r]) + ... + y_{K-1}[r]) / div) * mul for r in [0, rows) — the
+ * additions and roundings of the INIT, ADD..., FINAL_ACC epilogue sequence (K == 1: FINAL_E), so
+ * bitwise what they give. e, out and the K (1..8) tables ys[k] (a HOST array of device pointers)
+ * are [rows, d] fp32, 16-byte aligned, d % 4 == 0. The reduce-mode forward keeps its reduced item
+ * rows per layer (the next user pass reads them anyway) and runs this once on its item share
+ * instead of one epilogue pass per layer over every item row (reference models/light_gcn.py:36). */
+int lgcn_stack_mean_rows(const float* e, const float* const* ys, int32_t K, int64_t rows, int32_t d, float* out,
+                         float div, float mul, lgcn_stream_t stream);
+
 /* out[i] = (in[i] * mul) / div over n floats: the gradient that MulBackward (× 1/(K+1))
  * then MeanBackward (÷ (K+1)) hand to every layer output (reference models/light_gcn.py:36). */
 int lgcn_scale(const float* in, float* out, int64_t n, float mul, float div, lgcn_stream_t stream);
@@ -384,7 +428,9 @@ int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, co
  * steps a row missed, when the row is next touched (reference utils/train_test.py:95-96; same
  * element arithmetic as lgcn_adam_step). Tables p/g/m/v are (lo, hi) split at `split` rows of d.
  *   lgcn_adam_consts: consts[t] = (float(-lr / (1 - beta1^t)), float(sqrt(1 - beta2^t))),
- *     t in [t0, t1] (float pairs), the lgcn_adam_prologue formulas.
+ *     t in [t0, t1] (float pairs), the lgcn_adam_prologue formulas; consts[0].x = 1 when beta2 is
+ *     exactly 0.999 (the schedule whose step-constant division lgcn_row_adam may take by Markstein's
+ *     proven-exact shortcut; set by a call with t0 = 1, cleared by a call with another beta2), else 0.
  *   lgcn_row_adam: rows = rows_a[0..n_a) then keys_b[j] + off_b (j counted only if first_b[j]
  *     and !skip_b[row], when those are given). *step = completed steps (device int64).
  *     mode 0: catch the rows up to *step (duplicates handled by claim stamps, claim initialised

@@ -58,29 +58,22 @@ __device__ __forceinline__ T* trow(T* lo, T* hi, int64_t split, int64_t r, int64
     return r < split ? lo + r * d : hi + (r - split) * d;
 }
 
-#ifndef LGCN_ADAM_EARLY_LAST
-#define LGCN_ADAM_EARLY_LAST 1
-#endif
-
-#ifndef LGCN_ADAM_MARKSTEIN
-#define LGCN_ADAM_MARKSTEIN 1
-#endif
-
 // sqrt(v) / c with c = bc2_sqrt, the step's constant, and rc = 1 / c (both fp32, rc correctly
 // rounded): Markstein's correction q0 = s * rc, r = fma(-c, q0, s) (exact), q = fma(r, rc, q0)
 // gives the correctly rounded quotient — the value IEEE division gives — in 3 instructions instead
 // of the division's 9 (v_div_scale x 2, v_rcp, 4 FMAs, v_div_fmas, v_div_fixup). Proven for the
 // schedule of beta2 = 0.999 (the reference's Adam default): tools/markstein_check.c tries every
 // significand of a binade — by scale invariance every normal s; s = sqrt(v) is never subnormal —
-// for each of its 10,030 distinct step constants, 0 mismatches (profiles/r03x_adam/). Any other
-// beta2 takes the IEEE division.
+// for each of its 10,030 distinct step constants, 0 mismatches (profiles/r03x_adam/). The proof
+// covers the constants built from the double beta2 = 0.999 exactly: lgcn_adam_consts records that in
+// consts[0].x (kConstsMarkstein), and k_row_adam takes the shortcut only when it is set; any other
+// beta2 — np.float32(0.999) passed as a double included — takes the IEEE division. That the device's
+// constants equal the checker's host-libm ones is a GPU test (test_gpu_training.py).
 __device__ __forceinline__ float div_step(float s, float c, float rc, int markstein) {
-#if LGCN_ADAM_MARKSTEIN
     if (markstein) {
         const float q0 = s * rc;
         return __builtin_fmaf(__builtin_fmaf(-c, q0, s), rc, q0);
     }
-#endif
     return s / c;
 }
 
@@ -106,21 +99,37 @@ __device__ __forceinline__ void adam_elem_zero(float& p, float& m, float& v, flo
     p = p + step_size * (m / denom);
 }
 
-__device__ __forceinline__ bool list_row(const RowList& L, int64_t i, int64_t& row) {
+// Entry i of the list: its row, and whether it passes the first_b filter. An entry that fails it
+// may be padding (ids -1 in the exchange's slot arrays), so `row` must not be dereferenced for it.
+__device__ __forceinline__ bool list_entry(const RowList& L, int64_t i, int64_t& row) {
     if (i < L.n_a) {
         row = L.rows_a[i];
         return true;
     }
     const int64_t j = i - L.n_a;
     row = L.keys_b[j] + L.off_b;
-    if (L.first_b && !L.first_b[j]) return false;
-    if (L.skip_b && L.skip_b[row]) return false;
-    return true;
+    return !L.first_b || L.first_b[j];
 }
+
+// ... and the skip_b filter (only for entries that passed list_entry: skip_b is indexed by row)
+__device__ __forceinline__ bool list_skipped(const RowList& L, int64_t i, int64_t row) {
+    return i >= L.n_a && L.skip_b && L.skip_b[row];
+}
+
+__device__ __forceinline__ bool list_row(const RowList& L, int64_t i, int64_t& row) {
+    return list_entry(L, i, row) && !list_skipped(L, i, row);
+}
+
+// consts[0].x: 1 when the constants come from the double beta2 = 0.999 exactly (the schedule
+// tools/markstein_check.c proves the div_step shortcut for), else 0. Set by a call starting at t = 1,
+// cleared by any call with another beta2.
+constexpr double kMarksteinBeta2 = 0.999;
 
 __global__ void k_adam_consts(float2* __restrict__ consts, int64_t t0, int64_t t1, float lr, double beta1,
                               double beta2) {
     const int64_t t = t0 + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (t0 == 1 || beta2 != kMarksteinBeta2))
+        consts[0] = make_float2(beta2 == kMarksteinBeta2 ? 1.0f : 0.0f, 0.0f);
     if (t > t1) return;
     const double bc1 = 1.0 - pow(beta1, double(t));
     const double bc2 = 1.0 - pow(beta2, double(t));
@@ -143,6 +152,7 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
     // mode 3: the update after lgcn_row_grad_norm already advanced the counter to t + 1
     const bool upd = mode == 1 || mode == 3;
     const int64_t t = step[0] - (mode == 3 ? 1 : 0);
+    if (consts[0].x != 1.0f) k.markstein = 0;  // constants not from the proven schedule
     int64_t row;
     int32_t last_row;
     if (mode == 2) {
@@ -151,13 +161,11 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
         last_row = last[row];
     } else {
         if (i >= L.n_a + L.n_b) return;
-        const bool listed = list_row(L, i, row);
-#if LGCN_ADAM_EARLY_LAST
-        // issued beside the list filters and the claim instead of after them: only this row's
+        if (!list_entry(L, i, row)) return;  // filtered (or padding: row may be -1)
+        // issued beside the skip filter and the claim instead of after them: only this row's
         // winner ever writes last[row] (its lane 0, at the end), so the value is the same
         last_row = last[row];
-#endif
-        if (!listed) return;
+        if (list_skipped(L, i, row)) return;
         if (mode == 0) {
             // duplicates in the catch-up list: the first claimer of this step's stamp does the work
             int won = 0;
@@ -166,9 +174,6 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
             if (!won) return;
         }
     }
-#if !LGCN_ADAM_EARLY_LAST
-    if (mode != 2) last_row = last[row];
-#endif
     const int64_t from = int64_t(last_row) + 1;
     const int64_t upto = t;  // zero-gradient replays through step t
     // a catch-up (or flush) of a row that is already current touches nothing (on the planted

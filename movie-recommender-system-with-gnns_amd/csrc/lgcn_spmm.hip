@@ -326,16 +326,17 @@ __device__ __forceinline__ void split_row_block(const SpmmArgs& a, int64_t s, in
 // running sum from a.run unless it is the row's FIRST segment, and runs the epilogue only on its
 // LAST one; the sum stays one sequential chain in CSR order across launches.
 // BSPLIT: workgroups [0, n_splits) sum the split rows (split_row_block), the rest the items.
-template <int LPR, int NV, int UNROLL, bool SLICED = false, int TAIL = 0, bool BSPLIT = false, int CM = 1>
-__global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
+// blk: the workgroup's index within this pass (blockIdx.x, or its share of a paired launch).
+template <int LPR, int NV, int UNROLL, bool SLICED, int TAIL, bool BSPLIT, int CM>
+__device__ __forceinline__ void item_pass(const SpmmArgs& a, int64_t blk) {
     constexpr int GPB = kBlock / LPR;
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
-    if (BSPLIT && int64_t(blockIdx.x) < a.n_splits) {
-        split_row_block<LPR, NV, UNROLL, TAIL, CM>(a, blockIdx.x, g, l);
+    if (BSPLIT && blk < a.n_splits) {
+        split_row_block<LPR, NV, UNROLL, TAIL, CM>(a, blk, g, l);
         return;
     }
-    const int64_t item = (int64_t(blockIdx.x) - (BSPLIT ? a.n_splits : 0)) * GPB + g;
+    const int64_t item = (blk - (BSPLIT ? a.n_splits : 0)) * GPB + g;
     if (item >= a.n_items) return;
     lgcn_item_t it = a.items[item];
     int32_t flags = kItemFirst | kItemLast;
@@ -369,19 +370,36 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
     finish_row_vec<LPR, NV>(a, it.dst, l, acc);
 }
 
+template <int LPR, int NV, int UNROLL, bool SLICED = false, int TAIL = 0, bool BSPLIT = false, int CM = 1>
+__global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
+    item_pass<LPR, NV, UNROLL, SLICED, TAIL, BSPLIT, CM>(a, blockIdx.x);
+}
+
+// Two independent plain item passes of one width in one launch (lgcn_spmm_pair): workgroups
+// [0, blocks_a) run pass a, the rest pass b. Each pass keeps its own longest-first order, and b's
+// longest items start while a's last workgroups drain, so the pair pays one launch gap and one
+// drain instead of two. Per row the arithmetic is the single pass's (bitwise).
+template <int LPR, int NV, int UNROLL, int TAIL, int CM>
+__global__ __launch_bounds__(kBlock) void k_spmm_pair(SpmmArgs a, SpmmArgs b, int64_t blocks_a) {
+    const int64_t blk = blockIdx.x;
+    if (blk < blocks_a)
+        item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(a, blk);
+    else
+        item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(b, blk - blocks_a);
+}
+
 // Split rows: one workgroup per split row. Running sum v (of kVSums, owned by lane group v % GPB)
 // adds partials v, v + kVSums, ... with UNROLL loads in flight; the kVSums sums are then added in
 // v order through LDS. The association is fixed by the code and the same at every width, so
 // results are deterministic run to run and a column share is bitwise the full row's share.
 template <int LPR, int NV>
-__global__ __launch_bounds__(kBlock) void k_combine_vec(SpmmArgs a) {
+__device__ __forceinline__ void combine_row(const SpmmArgs& a, int64_t s) {
     constexpr int GPB = kBlock / LPR;
     constexpr int VPG = (kVSums + GPB - 1) / GPB;
     constexpr int UNROLL = 4;
     __shared__ float4 lds[kVSums][LPR * NV];
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
-    const int64_t s = blockIdx.x;
     if (s >= a.n_splits) return;  // whole block
     const lgcn_split_t sp = a.splits[s];
     const int64_t d4 = int64_t(LPR) * NV;
@@ -421,6 +439,21 @@ __global__ __launch_bounds__(kBlock) void k_combine_vec(SpmmArgs a) {
 #pragma unroll
         for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], lds[h][l + k * LPR]);
     finish_row_vec<LPR, NV>(a, sp.row, l, acc);
+}
+
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_combine_vec(SpmmArgs a) {
+    combine_row<LPR, NV>(a, blockIdx.x);
+}
+
+// The split rows of two passes in one launch: workgroups [0, a.n_splits) combine a's, the rest b's.
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_combine_pair(SpmmArgs a, SpmmArgs b) {
+    const int64_t s = blockIdx.x;
+    if (s < a.n_splits)
+        combine_row<LPR, NV>(a, s);
+    else
+        combine_row<LPR, NV>(b, s - a.n_splits);
 }
 
 // ---- generic path: any d <= 64*KMAX, one wave per item, scalar columns ----
@@ -498,8 +531,22 @@ __global__ __launch_bounds__(kBlock) void k_combine_scalar(SpmmArgs a) {
 enum { PASS_ITEMS = 1, PASS_COMBINE = 2, PASS_BOTH = 3, PASS_BSPLIT = 4 };
 
 template <int LPR, int NV, int UNROLL, int TAIL = 0, int CM = 1>
-int launch_vec(const SpmmArgs& a, hipStream_t s, int pass) {
+int launch_vec(const SpmmArgs& a, hipStream_t s, int pass, const SpmmArgs* b = nullptr) {
     constexpr int GPB = kBlock / LPR;
+    if (b != nullptr) {  // lgcn_spmm_pair: two plain passes, one launch per half
+        if (pass & PASS_ITEMS) {
+            const int64_t ba = (a.n_items + GPB - 1) / GPB, bb = (b->n_items + GPB - 1) / GPB;
+            if (ba + bb > 0) {
+                k_spmm_pair<LPR, NV, UNROLL, TAIL, CM><<<dim3(static_cast<unsigned>(ba + bb)), kBlock, 0, s>>>(a, *b, ba);
+                if (int rc = check_launch("k_spmm_pair")) return rc;
+            }
+        }
+        if ((pass & PASS_COMBINE) && a.n_splits + b->n_splits > 0) {
+            k_combine_pair<LPR, NV><<<dim3(static_cast<unsigned>(a.n_splits + b->n_splits)), kBlock, 0, s>>>(a, *b);
+            if (int rc = check_launch("k_combine_pair")) return rc;
+        }
+        return LGCN_OK;
+    }
     if (pass == PASS_BSPLIT) {  // split rows (one workgroup each) and items in one launch
         const int64_t blocks = a.n_splits + (a.n_items + GPB - 1) / GPB;
         if (blocks > 0) {
@@ -558,6 +605,21 @@ __global__ void k_scale(const float* __restrict__ in, float* __restrict__ out, i
         out[i] = (in[i] * mul) / div;
 }
 
+// out[r] = (((e[r] + y0[r]) + y1[r]) + ... + y_{K-1}[r]) / div * mul (K == 1: (e + y0) / div * mul):
+// the same roundings in the same order as the INIT / ADD / FINAL_ACC (FINAL_E) epilogues.
+struct StackRows {
+    const float* y[8];
+};
+__global__ void k_stack_mean(const float4* __restrict__ e, StackRows ys, int32_t K, int64_t n4, float4* __restrict__ out,
+                             float div, float mul) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 acc = e[i];
+        for (int k = 0; k < K; ++k) acc = f4_add(acc, reinterpret_cast<const float4*>(ys.y[k])[i]);
+        out[i] = f4_divmul(acc, div, mul);
+    }
+}
+
 __global__ void k_copy_scale(const float* __restrict__ lo, const float* __restrict__ hi, int64_t split,
                              int64_t N, int32_t d, float* __restrict__ out, float div, float mul) {
     const int64_t n = N * d;
@@ -570,12 +632,11 @@ __global__ void k_copy_scale(const float* __restrict__ lo, const float* __restri
     }
 }
 
-int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* splits, int64_t n_splits,
-              const int32_t* col, const float* val, int64_t N, int32_t d, const float* x_lo,
-              const float* x_hi, int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split,
-              float* y, float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
-              float div, float mul, lgcn_stream_t stream, int pass, float* run = nullptr,
-              const lgcn_item_t* chunks = nullptr) {
+// Argument checks of one pass (everything but the empty-pass shortcut); LGCN_OK or the failure.
+int check_pass(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* splits, int64_t n_splits, int64_t N,
+               int32_t d, const float* x_lo, const float* x_hi, int64_t x_split, const float* e_lo, const float* e_hi,
+               int64_t e_split, const float* acc_lo, const float* acc_hi, int64_t acc_split, const float* partial,
+               int32_t mode, int pass, const lgcn_item_t* chunks) {
     if (N < 0 || d <= 0 || n_items < 0 || n_splits < 0)
         return fail(LGCN_E_ARG, "lgcn_spmm: bad sizes (N=%lld d=%d)", (long long)N, d);
     if (mode < LGCN_EPI_INIT || mode > LGCN_EPI_SCALE) return fail(LGCN_E_ARG, "lgcn_spmm: bad mode %d", mode);
@@ -595,10 +656,38 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
     }
     if (d > 64 * KMAX && d % 4 != 0)
         return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm: d=%d unsupported (d > %d needs d %% 4 == 0)", d, 64 * KMAX);
+    return LGCN_OK;
+}
 
+bool vec_aligned(const SpmmArgs& a) {
+    return (a.d % 4 == 0) && aligned16(a.x_lo) && aligned16(a.acc_lo) && aligned16(a.partial) &&
+           (a.x_hi == nullptr || aligned16(a.x_hi)) && (a.acc_hi == nullptr || aligned16(a.acc_hi)) &&
+           (a.e_lo == nullptr || aligned16(a.e_lo)) && (a.e_hi == nullptr || aligned16(a.e_hi)) &&
+           (a.y == nullptr || aligned16(a.y));
+}
+
+int dispatch(SpmmArgs& a, int64_t N, hipStream_t s, int pass, float* run, const SpmmArgs* b);
+
+int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* splits, int64_t n_splits,
+              const int32_t* col, const float* val, int64_t N, int32_t d, const float* x_lo,
+              const float* x_hi, int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split,
+              float* y, float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
+              float div, float mul, lgcn_stream_t stream, int pass, float* run = nullptr,
+              const lgcn_item_t* chunks = nullptr) {
+    if (int rc = check_pass(items, n_items, splits, n_splits, N, d, x_lo, x_hi, x_split, e_lo, e_hi, e_split, acc_lo,
+                            acc_hi, acc_split, partial, mode, pass, chunks))
+        return rc;
+    if (N == 0 || (n_items == 0 && n_splits == 0)) return LGCN_OK;
     SpmmArgs a{items, n_items, splits, n_splits, col, val, x_lo, x_hi, x_split, e_lo, e_hi, e_split,
                y, acc_lo, acc_hi, acc_split, partial, d, mode, div, mul, run, chunks};
-    hipStream_t s = as_stream(stream);
+    return dispatch(a, N, as_stream(stream), pass, run, nullptr);
+}
+
+// The kernel instance for width d (and the launch's kind), launched for pass a — or for the pair
+// (a, b) of lgcn_spmm_pair, which share d, N and the instance.
+int dispatch(SpmmArgs& a, int64_t N, hipStream_t s, int pass, float* run, const SpmmArgs* b) {
+    const int32_t d = a.d;
+    const int64_t n_items = a.n_items + (b ? b->n_items : 0);
     // Non-temporal row traffic (epilogue e/acc/y and running-sum loads and stores): those rows are
     // touched once per launch, so they stream past the L2 and leave it to the gathered rows.
     // Measured (profiles/r02z_nt/): sliced C2 K=3 d=64 1.274 -> 1.241 ms, d=32 0.747 -> 0.698. On
@@ -607,11 +696,15 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
     // y is the next layer's gathered table) — and for block-split Cluster-GCN launches (+2.6 %).
     a.nt = (pass != PASS_BSPLIT && (run != nullptr || N * int64_t(d) * 4 > (int64_t(512) << 20))) ? 3 : 0;
     if (const char* nt = std::getenv("LGCN_SPMM_NT")) a.nt = std::atoi(nt);
+    SpmmArgs bb;
+    if (b != nullptr) {
+        bb = *b;
+        bb.nt = a.nt;
+        b = &bb;
+    }
 
-    bool vec_ok = (d % 4 == 0) && aligned16(x_lo) && aligned16(acc_lo) && aligned16(partial) &&
-                  (x_hi == nullptr || aligned16(x_hi)) && (acc_hi == nullptr || aligned16(acc_hi)) &&
-                  (e_lo == nullptr || aligned16(e_lo)) && (e_hi == nullptr || aligned16(e_hi)) &&
-                  (y == nullptr || aligned16(y));
+    const bool vec_ok = vec_aligned(a) && (b == nullptr || vec_aligned(*b));
+    if (b != nullptr && !vec_ok) return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm_pair: needs d in {4,8,...,1024} and aligned rows");
     if (vec_ok) {
         // Predicated tail (TAIL = 1): a row's last < UNROLL edges of each batch are gathered
         // together instead of one at a time. It costs VGPRs (occupancy 6-7 -> 4 waves/SIMD at
@@ -632,45 +725,45 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
         const int cm = spmm_cm();
         if (tail) {
             switch (d) {
-                case 4: return (cm ? cm : rounds ? 32 : 8) == 32 ? launch_vec<1, 1, 8, 1, 32>(a, s, pass)
-                                                                : launch_vec<1, 1, 8, 1, 8>(a, s, pass);
+                case 4: return (cm ? cm : rounds ? 32 : 8) == 32 ? launch_vec<1, 1, 8, 1, 32>(a, s, pass, b)
+                                                                : launch_vec<1, 1, 8, 1, 8>(a, s, pass, b);
                 case 8: {
                     const int c = cm ? cm : rounds ? 32 : 4;
-                    return c == 16 ? launch_vec<2, 1, 8, 1, 16>(a, s, pass)
-                         : c == 32 ? launch_vec<2, 1, 8, 1, 32>(a, s, pass) : launch_vec<2, 1, 8, 1, 4>(a, s, pass);
+                    return c == 16 ? launch_vec<2, 1, 8, 1, 16>(a, s, pass, b)
+                         : c == 32 ? launch_vec<2, 1, 8, 1, 32>(a, s, pass, b) : launch_vec<2, 1, 8, 1, 4>(a, s, pass, b);
                 }
                 case 16: {
                     const int c = cm ? cm : rounds ? 16 : 2;
-                    return c == 8 ? launch_vec<4, 1, 8, 1, 8>(a, s, pass)
-                         : c == 16 ? launch_vec<4, 1, 8, 1, 16>(a, s, pass) : launch_vec<4, 1, 8, 1, 2>(a, s, pass);
+                    return c == 8 ? launch_vec<4, 1, 8, 1, 8>(a, s, pass, b)
+                         : c == 16 ? launch_vec<4, 1, 8, 1, 16>(a, s, pass, b) : launch_vec<4, 1, 8, 1, 2>(a, s, pass, b);
                 }
                 case 32: {
                     const int c = cm ? cm : rounds ? 4 : 1;
-                    return c == 4 ? launch_vec<8, 1, 8, 1, 4>(a, s, pass)
-                         : c == 8 ? launch_vec<8, 1, 8, 1, 8>(a, s, pass) : launch_vec<8, 1, 8, 1>(a, s, pass);
+                    return c == 4 ? launch_vec<8, 1, 8, 1, 4>(a, s, pass, b)
+                         : c == 8 ? launch_vec<8, 1, 8, 1, 8>(a, s, pass, b) : launch_vec<8, 1, 8, 1>(a, s, pass, b);
                 }
                 case 64: {
                     const int c = cm ? cm : rounds ? 4 : 1;
-                    return c == 4 ? launch_vec<16, 1, 8, 1, 4>(a, s, pass)
-                         : c == 2 ? launch_vec<16, 1, 8, 1, 2>(a, s, pass) : launch_vec<16, 1, 8, 1>(a, s, pass);
+                    return c == 4 ? launch_vec<16, 1, 8, 1, 4>(a, s, pass, b)
+                         : c == 2 ? launch_vec<16, 1, 8, 1, 2>(a, s, pass, b) : launch_vec<16, 1, 8, 1>(a, s, pass, b);
                 }
-                case 128: return launch_vec<32, 1, 8, 1>(a, s, pass);
-                case 256: return launch_vec<64, 1, 8, 1>(a, s, pass);
-                case 512: return launch_vec<64, 2, 4, 1>(a, s, pass);
-                case 1024: return launch_vec<64, 4, 2, 1>(a, s, pass);
+                case 128: return launch_vec<32, 1, 8, 1>(a, s, pass, b);
+                case 256: return launch_vec<64, 1, 8, 1>(a, s, pass, b);
+                case 512: return launch_vec<64, 2, 4, 1>(a, s, pass, b);
+                case 1024: return launch_vec<64, 4, 2, 1>(a, s, pass, b);
                 default: break;
             }
         }
         switch (d) {
-            case 4: return launch_vec<1, 1, 8, 0, 8>(a, s, pass);
-            case 8: return launch_vec<2, 1, 8, 0, 4>(a, s, pass);
-            case 16: return launch_vec<4, 1, 8, 0, 2>(a, s, pass);
-            case 32: return launch_vec<8, 1, 8>(a, s, pass);
-            case 64: return v == 1 ? launch_vec<16, 1, 16>(a, s, pass) : launch_vec<16, 1, 8>(a, s, pass);
-            case 128: return launch_vec<32, 1, 8>(a, s, pass);
-            case 256: return launch_vec<64, 1, 8>(a, s, pass);
-            case 512: return launch_vec<64, 2, 4>(a, s, pass);
-            case 1024: return launch_vec<64, 4, 2>(a, s, pass);
+            case 4: return launch_vec<1, 1, 8, 0, 8>(a, s, pass, b);
+            case 8: return launch_vec<2, 1, 8, 0, 4>(a, s, pass, b);
+            case 16: return launch_vec<4, 1, 8, 0, 2>(a, s, pass, b);
+            case 32: return launch_vec<8, 1, 8>(a, s, pass, b);
+            case 64: return v == 1 ? launch_vec<16, 1, 16>(a, s, pass, b) : launch_vec<16, 1, 8>(a, s, pass, b);
+            case 128: return launch_vec<32, 1, 8>(a, s, pass, b);
+            case 256: return launch_vec<64, 1, 8>(a, s, pass, b);
+            case 512: return launch_vec<64, 2, 4>(a, s, pass, b);
+            case 1024: return launch_vec<64, 4, 2>(a, s, pass, b);
             default: break;
         }
     }
@@ -721,6 +814,42 @@ int lgcn_spmm_run_slices(const lgcn_item_t* items, const int64_t* slice_offsets,
 }
 int lgcn_spmm_blocksplit(LGCN_SPMM_PARAMS, const lgcn_item_t* chunks) {
     return spmm_impl(LGCN_SPMM_ARGS, PASS_BSPLIT, nullptr, chunks);
+}
+
+int lgcn_spmm_pair(const lgcn_pass_t* a, const lgcn_pass_t* b, int64_t N, int32_t d, int32_t what,
+                   lgcn_stream_t stream) {
+    if (!a || !b || what < 1 || what > 3) return fail(LGCN_E_ARG, "lgcn_spmm_pair: bad args");
+    const lgcn_pass_t* ps[2] = {a, b};
+    SpmmArgs args[2];
+    for (int i = 0; i < 2; ++i) {
+        const lgcn_pass_t& p = *ps[i];
+        if (int rc = check_pass(p.items, p.n_items, p.splits, p.n_splits, N, d, p.x_lo, p.x_hi, p.x_split, p.e_lo,
+                                p.e_hi, p.e_split, p.acc_lo, p.acc_hi, p.acc_split, p.partial, p.mode, PASS_BOTH,
+                                nullptr))
+            return rc;
+        args[i] = SpmmArgs{p.items, p.n_items, p.splits, p.n_splits, p.col, p.val, p.x_lo, p.x_hi, p.x_split,
+                           p.e_lo, p.e_hi, p.e_split, p.y, p.acc_lo, p.acc_hi, p.acc_split, p.partial, d, p.mode,
+                           p.div, p.mul, nullptr, nullptr};
+    }
+    if (N == 0) return LGCN_OK;
+    return dispatch(args[0], N, as_stream(stream), what, nullptr, &args[1]);
+}
+
+int lgcn_stack_mean_rows(const float* e, const float* const* ys, int32_t K, int64_t rows, int32_t d, float* out,
+                         float div, float mul, lgcn_stream_t stream) {
+    if (K < 1 || K > 8 || rows < 0 || d <= 0 || d % 4 != 0 || (rows > 0 && (!e || !ys || !out)))
+        return fail(LGCN_E_ARG, "lgcn_stack_mean_rows: bad args (K=%d rows=%lld d=%d)", K, (long long)rows, d);
+    if (rows == 0) return LGCN_OK;
+    StackRows st{};
+    for (int k = 0; k < K; ++k) {
+        if (!ys[k] || !aligned16(ys[k])) return fail(LGCN_E_ARG, "lgcn_stack_mean_rows: layer %d table", k);
+        st.y[k] = ys[k];
+    }
+    if (!aligned16(e) || !aligned16(out)) return fail(LGCN_E_UNSUPPORTED, "lgcn_stack_mean_rows: alignment");
+    const int64_t n4 = rows * d / 4;
+    k_stack_mean<<<grid_for(n4, kBlock, 16384), kBlock, 0, as_stream(stream)>>>(
+        reinterpret_cast<const float4*>(e), st, K, n4, reinterpret_cast<float4*>(out), div, mul);
+    return check_launch("k_stack_mean");
 }
 
 int lgcn_scale(const float* in, float* out, int64_t n, float mul, float div, lgcn_stream_t stream) {

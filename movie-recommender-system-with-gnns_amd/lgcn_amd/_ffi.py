@@ -25,7 +25,7 @@ E_ARG, E_WORKSPACE, E_UNSUPPORTED = -1, -2, -3  # include/lgcn.h LGCN_E_*
 
 ITEM_BYTES = 16   # lgcn_item_t {int64 beg; int32 len; int32 dst}
 SPLIT_BYTES = 16  # lgcn_split_t {int32 row, pbeg, pcnt, pad}
-ABI_VERSION = 4  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
+ABI_VERSION = 5  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
 
 _lib = None
 
@@ -67,6 +67,8 @@ _SIGS = {
     "lgcn_spmm_blocksplit": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
                               _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp],
                              ctypes.c_int),
+    "lgcn_spmm_pair": ([_vp, _vp, _i64, _i32, _i32, _vp], ctypes.c_int),
+    "lgcn_stack_mean_rows": ([_vp, _vp, _i32, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_scale": ([_vp, _vp, _i64, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_copy_scale": ([_vp, _vp, _i64, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_bpr_fused": ([_vp, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _f32, _f32, _f32, _vp, _vp,
@@ -129,6 +131,17 @@ EXPORTED = tuple(_SIGS)
 class AdamTensor(ctypes.Structure):
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
                 ("exp_avg_sq", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+
+class Pass(ctypes.Structure):
+    """lgcn_pass_t: one lgcn_spmm pass's arguments (lgcn_spmm_pair)."""
+    _fields_ = [("items", ctypes.c_void_p), ("n_items", ctypes.c_int64), ("splits", ctypes.c_void_p),
+                ("n_splits", ctypes.c_int64), ("col", ctypes.c_void_p), ("val", ctypes.c_void_p),
+                ("x_lo", ctypes.c_void_p), ("x_hi", ctypes.c_void_p), ("x_split", ctypes.c_int64),
+                ("e_lo", ctypes.c_void_p), ("e_hi", ctypes.c_void_p), ("e_split", ctypes.c_int64),
+                ("y", ctypes.c_void_p), ("acc_lo", ctypes.c_void_p), ("acc_hi", ctypes.c_void_p),
+                ("acc_split", ctypes.c_int64), ("partial", ctypes.c_void_p), ("mode", ctypes.c_int32),
+                ("div", ctypes.c_float), ("mul", ctypes.c_float)]
 
 
 class LgcnError(RuntimeError):

@@ -164,8 +164,13 @@ class RowLazyAdam:
 
     # --- the owner-sharded exchange's pieces (lgcn_amd.owner): the clip norm over every rank's rows
     def sqnorm_partials(self, keys_b: torch.Tensor, skip_b: torch.Tensor, partials: torch.Tensor) -> None:
-        """Block partials of the sum of squares of the gradient rows keys_b[j] with !skip_b[row]."""
+        """Block partials of the sum of squares of the gradient rows keys_b[j] with !skip_b[row].
+        partials must hold lgcn_row_grad_norm_workspace_floats() floats (the kernel writes that many)."""
         lib = _ffi.load()
+        need = lib.lgcn_row_grad_norm_workspace_floats()
+        if partials.numel() < need or not partials.is_contiguous() or partials.dtype != torch.float32:
+            raise ValueError(f"sqnorm_partials: partials must be {need} contiguous fp32, got "
+                             f"{partials.numel()} {partials.dtype}")
         _ffi.check(lib.lgcn_row_grad_sqnorm(self.gu.data_ptr(), self.gi.data_ptr(), self.U, self.d, None, 0,
                                             keys_b.data_ptr(), keys_b.numel(), 0, None, skip_b.data_ptr(),
                                             partials.data_ptr(), _ffi.stream_of(self.device)),

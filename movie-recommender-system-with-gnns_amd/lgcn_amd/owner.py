@@ -92,6 +92,11 @@ class OwnerExchange:
         self.owned = torch.arange(self.rank, self.N, W, dtype=torch.int64, device=device)
         self.not_union = torch.ones(self.N, dtype=torch.uint8, device=device)
         self.norm_parts = int(norm_parts)
+        if torch.device(device).type == "cuda":
+            # lgcn_row_grad_sqnorm writes exactly this many block partials (no size argument)
+            need = _ffi.load().lgcn_row_grad_norm_workspace_floats()
+            if self.norm_parts != need:
+                raise ValueError(f"OwnerExchange: norm_parts={self.norm_parts} != the kernel's {need} partials")
         self.partials = torch.zeros(self.norm_parts, dtype=torch.float32, device=device)
         self.partials_all = torch.zeros(W * self.norm_parts, dtype=torch.float32, device=device)
         self.nccl = W > 1 and device_collectives()

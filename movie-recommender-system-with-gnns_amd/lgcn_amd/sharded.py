@@ -187,8 +187,8 @@ def grid_candidates(world: int, d: int, bipartite: bool = True,
             out.append((R, F, None))
         else:
             out += [(R, F, m) for m in (EXCHANGE_MODES if R >= 3 else EXCHANGE_MODES[:1])]
-            if bipartite:  # users sharded, item rows all-reduced (ReducePlan)
-                out.append((R, F, "reduce"))
+            if bipartite:  # users sharded, item rows all-reduced (ReducePlan), overlapped or fused order
+                out += [(R, F, "reduce"), (R, F, "reduce-fused")]
     if any(F > 1 for _, F, _ in out) and world < 4:
         out = [c for c in out if c[1] > 1]
     # the peer-send candidates last: batch_isend_irecv is the one exchange outside RCCL's plain
@@ -492,9 +492,14 @@ def propagate_forward_sharded(x0p: torch.Tensor, splan, K: int, exchange: BlockE
 #   — the one-GPU plain schedule's rows, from the full item table of layer k-1;
 # * item rows of layer k: each rank sums, for EVERY item, the in-edges whose source user it owns
 #   (a CSR of that edge subset with the whole graph's gcn_norm weights); the R partial tables are
-#   summed by one all_reduce per layer (RCCL, on a side stream, overlapped with the other half and
-#   the next layer's partial pass), then the LightGCN epilogue runs on the reduced item rows
-#   (an identity pass through lgcn_spmm: weight-1 self edges, so it is the same epilogue code).
+#   summed by one all_reduce per layer (RCCL, on a side stream, overlapped with the user pass);
+#   the reduced rows of every layer are kept (the next user pass reads them anyway), and the
+#   LightGCN layer-stack mean of the item rows runs once, at the end, on the rank's item share
+#   (lgcn_stack_mean_rows: the INIT / ADD / FINAL_ACC epilogues' additions in their order).
+# * "fused" (round 4): a layer's item-partial pass and user pass are independent (both read layer
+#   k-1), so they can run as ONE launch (lgcn_spmm_pair) and their split-row combines as one more;
+#   the layer's all_reduce then starts after both and the next layer waits for it (no overlap, one
+#   launch gap and one drain per pair instead of two). Both orders are timed grid candidates.
 #
 # Exchange per rank per K-layer step: K all_reduces of I x d/F floats (a ring moves 2 (R-1)/R of
 # it), instead of K-1 all_gathers of (R-1)/R of N x d/F. C2 at 8 x 1: 3 x 26.4 MB vs 2 x 52 MB;
@@ -527,25 +532,9 @@ class UserShards:
         return int(self.ub[g]), int(self.ub[g + 1])
 
 
-def _identity_items(U: int, N: int, dev, chunk: int, stream, rows: tuple[int, int] | None = None) -> object:
-    """The plain schedule of weight-1 self edges on the item rows (the item epilogue pass), or on
-    the item rows [U + a, U + b) only."""
-    from .plan import CsrDirection, _schedule
-
-    I = N - U
-    rowptr = torch.cat([torch.zeros(U, dtype=torch.int64), torch.arange(I + 1, dtype=torch.int64)]).to(dev)
-    col = torch.arange(U, N, dtype=torch.int32, device=dev)
-    eid = torch.arange(I, dtype=torch.int32, device=dev)
-    val = torch.ones(I, dtype=torch.float32, device=dev)
-    mask = torch.zeros(N, dtype=torch.uint8, device=dev)
-    a, b = rows if rows is not None else (0, I)
-    mask[U + a:U + b] = 1
-    return CsrDirection(rowptr, col, eid, val, *_schedule(rowptr, N, I, chunk, U, mask, stream), chunk)
-
-
 class ReducePlan:
-    """Row group g's plans for the reduce mode (see above): its users' rows over the whole CSR, the
-    item partials over the edges its users source, and the item epilogue pass."""
+    """Row group g's plans for the reduce mode (see above): its users' rows over the whole CSR and
+    the item partials over the edges its users source."""
 
     def __init__(self, edge_index: torch.Tensor, shards: UserShards, g: int, d: int, chunk: int | None = None):
         from .plan import DEFAULT_CHUNK, CsrDirection, _build_direction, _schedule
@@ -580,14 +569,12 @@ class ReducePlan:
         self.partial, _, _ = _build_direction(dst[sel].contiguous(), src[sel].contiguous(), N, self.chunk, U,
                                               self.dis, stream, items)
         self.partial.block_split = False
-        self.identity = _identity_items(U, N, dev, self.chunk, stream)
         # the last layer's item rows are reduce-scattered: this group's share of the items
         # (I padded to a multiple of R; padding rows are zero partials that no pass writes)
         R = shards.R
         self.I_pad = -(-shards.I // R) * R
         per = self.I_pad // R
         self.share = (min(shards.I, self.g * per), min(shards.I, (self.g + 1) * per))
-        self.identity_share = _identity_items(U, N, dev, self.chunk, stream, self.share)
         self.n_sub = int(sel.sum().item())
         self.scratch = {}
 
@@ -612,18 +599,43 @@ class ReducePlan:
         N, U = self.shards.N, self.shards.U
         spmm(self.users, N, self.d, (x_items, x_items, U), e, acc, y, mode, div, mul, self._part(self.users, self.d))
 
-    def run_item_epilogue(self, v_items: torch.Tensor, e, acc, mode: int, div: float, mul: float,
-                          share: bool = False) -> None:
-        """v_items: the reduced item rows (all of them), or with share=True this group's share only
-        (row U + a of the share at v_items[0])."""
-        from .propagate import spmm
+    def run_pair(self, x_users: torch.Tensor, part_items: torch.Tensor, x_items: torch.Tensor, e, acc, y, mode: int,
+                 div: float, mul: float) -> None:
+        """run_partial and run_users of one layer as two launches (lgcn_spmm_pair: both item passes
+        in one, both combines in the other) — the same per-row arithmetic."""
+        import ctypes
 
-        N, U = self.shards.N, self.shards.U
-        if share:
-            spmm(self.identity_share, N, self.d, (v_items, v_items, U + self.share[0]), e, acc, None, mode, div, mul,
-                 None)
-        else:
-            spmm(self.identity, N, self.d, (v_items, v_items, U), e, acc, None, mode, div, mul, None)
+        N, U, d = self.shards.N, self.shards.U, self.d
+        lib = _ffi.load()
+        el, eh, es = e if e is not None else (None, None, N)
+
+        def pass_of(direction, x, ee, y_, a_lo, a_hi, a_split, m, dv, ml):
+            part = self._part(direction, d)
+            return _ffi.Pass(direction.items.data_ptr(), direction.n_items, direction.splits.data_ptr(),
+                             direction.n_splits, direction.col.data_ptr(), direction.val.data_ptr(),
+                             _ffi.ptr(x[0]), _ffi.ptr(x[1]), x[2], _ffi.ptr(ee[0]), _ffi.ptr(ee[1]), ee[2],
+                             _ffi.ptr(y_), _ffi.ptr(a_lo), _ffi.ptr(a_hi), a_split, _ffi.ptr(part), m, dv, ml)
+
+        pa = pass_of(self.partial, (x_users, part_items, U), (None, None, N), None, part_items, part_items, U,
+                     _ffi.EPI_STORE, 1.0, 1.0)
+        pb = pass_of(self.users, (x_items, x_items, U), (el, eh, es), y, acc[0], acc[1], acc[2], mode, div, mul)
+        _ffi.check(lib.lgcn_spmm_pair(ctypes.byref(pa), ctypes.byref(pb), N, d, 3, _ffi.stream_of(x_users.device)),
+                   "lgcn_spmm_pair")
+
+    def finish_items(self, x0i: torch.Tensor, layers: list, last_share: torch.Tensor, out_i: torch.Tensor,
+                     div: float, mul: float) -> None:
+        """out_i[a:b] = the layer-stack mean of this group's item share [a, b): x0i, the reduced rows
+        of layers 1..K-1 (layers, all items) and layer K's share (last_share, row a at row 0)."""
+        a, b = self.share
+        if b <= a:
+            return
+        import ctypes
+
+        ys = [t[a:b] for t in layers] + [last_share[:b - a]]
+        arr = (ctypes.c_void_p * len(ys))(*[t.data_ptr() for t in ys])
+        _ffi.check(_ffi.load().lgcn_stack_mean_rows(x0i[a:b].data_ptr(), arr, len(ys), b - a, self.d,
+                                                    out_i[a:b].data_ptr(), div, mul,
+                                                    _ffi.stream_of(x0i.device)), "lgcn_stack_mean_rows")
 
 
 class ItemReducer:
@@ -689,16 +701,18 @@ class ItemReducer:
 
 
 def propagate_forward_reduced(x0u: torch.Tensor, x0i: torch.Tensor, rplan, K: int,
-                              reducer: ItemReducer) -> tuple[torch.Tensor, torch.Tensor]:
+                              reducer: ItemReducer, fused: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
     """(users [U, d], items [I, d]): the LightGCN final embedding of this row group's users and of
     its share of the items, rplan.share = [a, b) (other rows unwritten). x0u / x0i: the layer-0
     tables (this rank's columns).
 
     Layer k: the item partials from the users of layer k-1 (own rows), their all_reduce started;
-    then the users of layer k from the items of layer k-1 (reduced one layer earlier); then, once
-    layer k-1's reduction has landed, its item epilogue. Each reduction overlaps a user pass and
-    the next partial pass. The last layer's partials are reduce-scattered (each group member gets
-    its share of the items: half a ring all_reduce's bytes) and only the share's epilogue runs."""
+    then, once layer k-1's reduction has landed, the users of layer k from the items of layer k-1.
+    Each reduction overlaps a user pass. fused=True runs a layer's two passes as one pair of
+    launches (lgcn_spmm_pair) and starts its reduction after them. The last layer's partials are
+    reduce-scattered (each group member gets its share of the items: half a ring all_reduce's
+    bytes); the reduced rows of every layer are kept, and the item rows' layer-stack mean runs once
+    on the share (rplan.finish_items)."""
     U, d = x0u.shape
     I = x0i.shape[0]
     dev = x0u.device
@@ -710,8 +724,9 @@ def propagate_forward_reduced(x0u: torch.Tensor, x0i: torch.Tensor, rplan, K: in
         return (x0u / div) * mul, (x0i / div) * mul
     yu = [torch.empty((U, d), dtype=torch.float32, device=dev) for _ in range(min(2, K - 1))]
     I_pad = getattr(rplan, "I_pad", I)
-    part = [torch.zeros((I_pad, d), dtype=torch.float32, device=dev) for _ in range(min(2, K))]
-    a, b = getattr(rplan, "share", (0, I))
+    # the reduced item rows of layers 1..K-1 (read by the next user pass and by the final mean),
+    # and layer K's partials (reduce-scattered into `share`); padding rows stay zero
+    part = [torch.zeros((I_pad, d), dtype=torch.float32, device=dev) for _ in range(K)]
     share = torch.empty((I_pad // max(1, reducer.R), d), dtype=torch.float32, device=dev)
     e = (x0u, x0i, U)
     acc = (out_u, out_i, U)
@@ -721,27 +736,30 @@ def propagate_forward_reduced(x0u: torch.Tensor, x0i: torch.Tensor, rplan, K: in
             return _ffi.EPI_FINAL_E
         return _ffi.EPI_INIT if k == 1 else (_ffi.EPI_ADD if k < K else _ffi.EPI_FINAL_ACC)
 
-    pending = None  # (handle, layer) of the reduction in flight
+    def start(k):
+        if k < K:
+            return reducer.start(part[k - 1])
+        return reducer.start_scatter(part[k - 1], share, rplan.g)  # the last layer: this member's share
+
+    pending = None  # the reduction in flight
     for k in range(1, K + 1):
         src_u = x0u if k == 1 else yu[(k - 2) % 2]
-        src_i = x0i if k == 1 else part[(k - 2) % 2]
+        src_i = x0i if k == 1 else part[k - 2]
         mode = mode_of(k)
         final = mode in (_ffi.EPI_FINAL_E, _ffi.EPI_FINAL_ACC)
-        pk = part[(k - 1) % 2]
-        rplan.run_partial(src_u, pk)
-        if k < K:
-            started = (reducer.start(pk), k)
-        else:  # the last layer: this member's share of the item rows only
-            started = (reducer.start_scatter(pk, share, rplan.g), k)
-        if pending is not None:  # layer k-1's items: reduced before this layer's users read them
-            reducer.wait(pending[0], dev)
-            m = mode_of(pending[1])
-            rplan.run_item_epilogue(part[(pending[1] - 1) % 2], e, acc, m, 1.0, 1.0)
         y = yu[(k - 1) % 2] if k < K else None
-        rplan.run_users(src_i, e if mode in (_ffi.EPI_INIT, _ffi.EPI_FINAL_E) else None, acc, y, mode,
-                        div if final else 1.0, mul if final else 1.0)
-        pending = started
-    reducer.wait(pending[0], dev)
-    if b > a:
-        rplan.run_item_epilogue(share, e, acc, mode_of(K), div, mul, share=True)
+        ue = e if mode in (_ffi.EPI_INIT, _ffi.EPI_FINAL_E) else None
+        udiv, umul = (div, mul) if final else (1.0, 1.0)
+        if fused:
+            reducer.wait(pending, dev)  # layer k-1's items: reduced before this layer's users read them
+            rplan.run_pair(src_u, part[k - 1], src_i, ue, acc, y, mode, udiv, umul)
+            pending = start(k)
+        else:
+            rplan.run_partial(src_u, part[k - 1])
+            started = start(k)
+            reducer.wait(pending, dev)
+            rplan.run_users(src_i, ue, acc, y, mode, udiv, umul)
+            pending = started
+    reducer.wait(pending, dev)
+    rplan.finish_items(x0i, part[:K - 1], share, out_i, div, mul)
     return out_u, out_i

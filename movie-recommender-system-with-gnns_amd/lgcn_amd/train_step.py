@@ -665,6 +665,12 @@ class FusedTrainStep:
         ex.pending = nxt
         self._synced = False
         self._k += 1
+        if not getattr(st, "owner_checked", False):
+            # the blocks are sized so that neither list can overflow (cap >= touched + B of every
+            # batch); the first step of each batch state checks that with one host read, so a
+            # dropped row is an error at once rather than at the next check_overflow()
+            ex.check_overflow()
+            st.owner_checked = True
         return loss
 
     def sync(self) -> None:

@@ -67,9 +67,30 @@ def compute_embeddings(model: torch.nn.Module, data, device) -> Tuple[torch.Tens
             items_final[n], items_0[n])
 
 
+# which step the last train() call ran: "fused" (lgcn_amd.harness) or "reference: <why not fused>"
+LAST_TRAIN_PATH = None
+
+
 def train(model: torch.nn.Module, optimizer: torch.optim.Optimizer, train_loader, device) -> float:
-    """One epoch over the loader; returns the edge-weighted mean batch loss (reference :66-103)."""
+    """One epoch over the loader; returns the edge-weighted mean batch loss (reference :66-103).
+    A HIP LightGCN with the reference's torch Adam runs the fused batch step (lgcn_amd.harness:
+    HIP forward / BPR / backward and the exact row-lazy Adam, one hipGraph per batch) with the
+    same negatives, loss and optimizer state; anything else runs the reference-style loop below."""
+    global LAST_TRAIN_PATH
     model.train()
+    why = "model not on a ROCm device"
+    weight = getattr(getattr(model, "user_embedding", None), "weight", None)
+    if weight is not None and weight.is_cuda:
+        from lgcn_amd import harness
+
+        why = harness.eligibility(model, optimizer)
+        if why is None:
+            res = harness.train_epoch(model, optimizer, train_loader, device)
+            if res is not None:
+                LAST_TRAIN_PATH = "fused"
+                return res[0] / res[1]
+            why = "a batch is not a bipartite user-item edge list"
+    LAST_TRAIN_PATH = f"reference: {why}"
     total_loss = None
     total_w = 0
     for batch in train_loader:

@@ -186,7 +186,7 @@ def _check_sharded_ranks(gpu, monkeypatch, tmp_path, case, world, F, mode, dc):
     assert sum(int(m[0]) for m in meta) == n_hubs
 
 
-def _reduce_worker(rank, world, port, case, out_dir, F=1, dc=False):
+def _reduce_worker(rank, world, port, case, out_dir, F=1, dc=False, fused=False):
     import sys
 
     from conftest import PKG, ROOT
@@ -213,7 +213,7 @@ def _reduce_worker(rank, world, port, case, out_dir, F=1, dc=False):
     rplan = ReducePlan(torch.from_numpy(ei).to(dev), shards, grid.row_group, c1 - c0, chunk)
     red = ItemReducer(grid.R, grid.exchange_group(dist))
     ou, oi = propagate_forward_reduced(torch.from_numpy(uw[:, c0:c1].copy()).to(dev),
-                                       torch.from_numpy(iw[:, c0:c1].copy()).to(dev), rplan, K, red)
+                                       torch.from_numpy(iw[:, c0:c1].copy()).to(dev), rplan, K, red, fused=fused)
     ua, ub = shards.users(grid.row_group)
     a, b = rplan.share
     np.save(os.path.join(out_dir, f"u{grid.row_group}_{grid.col_group}.npy"), ou[ua:ub].cpu().numpy())
@@ -238,7 +238,23 @@ def test_reduce_mode_device_collectives(gpu, tmp_path, case, world, F):
     _check_reduce_ranks(gpu, tmp_path, case, world, F, True)
 
 
-def _check_reduce_ranks(gpu, tmp_path, case, world, F, dc):
+@pytest.mark.parametrize("case,world,F", [("ml25m5_plain", 4, 2), ("ml25m5_sliced", 8, 1), ("sub_K2_d128", 2, 1)])
+def test_reduce_mode_fused_pairs(gpu, tmp_path, case, world, F):
+    """The fused order (a layer's partial and user passes as one lgcn_spmm_pair launch, their combines
+    as another) within 1e-5 of the oracle, and bitwise the overlapped order's output."""
+    fused_dir = tmp_path / "fused"
+    fused_dir.mkdir()
+    _check_reduce_ranks(gpu, fused_dir, case, world, F, False, fused=True)
+    plain_dir = tmp_path / "plain"
+    plain_dir.mkdir()
+    _check_reduce_ranks(gpu, plain_dir, case, world, F, False)
+    files = sorted(p.name for p in fused_dir.glob("*.npy"))
+    assert files and files == sorted(p.name for p in plain_dir.glob("*.npy"))
+    for f in files:
+        assert np.array_equal(np.load(fused_dir / f), np.load(plain_dir / f)), f
+
+
+def _check_reduce_ranks(gpu, tmp_path, case, world, F, dc, fused=False):
     import graphs
     from oracle import c_oracle
     from parity import assert_rows_close
@@ -250,7 +266,7 @@ def _check_reduce_ranks(gpu, tmp_path, case, world, F, dc):
     uw, iw = graphs.embeddings(U, I, d, seed=K + d)
     ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
     torch.cuda.synchronize()
-    mp.spawn(_reduce_worker, args=(world, _free_port(), case, str(tmp_path), F, dc), nprocs=world, join=True)
+    mp.spawn(_reduce_worker, args=(world, _free_port(), case, str(tmp_path), F, dc, fused), nprocs=world, join=True)
     R = world // F
     shards = UserShards.build(np.bincount(ei[1], minlength=U + I), U, R)
     w = d // F

@@ -203,14 +203,15 @@ def test_grid_candidates():
     assert grid_candidates(2, 64) == [(1, 2, None)]
     # world >= 4: R - 1 >= 3 links; "reduce" (users sharded, items all-reduced) for every R > 1
     # peer sends (p2p) are timed after every other candidate (a hang there cannot stop the others)
-    rows_only = lambda w: [(w, 1, "allgather"), (w, 1, "reduce")]  # noqa: E731
-    assert grid_candidates(4, 64) == [(1, 4, None), (2, 2, "allgather"), (2, 2, "reduce")] + rows_only(4) + \
+    red = lambda R, F: [(R, F, "reduce"), (R, F, "reduce-fused")]  # noqa: E731
+    rows_only = lambda w: [(w, 1, "allgather")] + red(w, 1)  # noqa: E731
+    assert grid_candidates(4, 64) == [(1, 4, None), (2, 2, "allgather")] + red(2, 2) + rows_only(4) + \
         [(4, 1, "p2p")]
-    assert grid_candidates(8, 64) == [(1, 8, None), (2, 4, "allgather"), (2, 4, "reduce"), (4, 2, "allgather"),
-                                      (4, 2, "reduce")] + rows_only(8) + [(4, 2, "p2p"), (8, 1, "p2p")]
+    assert grid_candidates(8, 64) == [(1, 8, None), (2, 4, "allgather")] + red(2, 4) + [(4, 2, "allgather")] + \
+        red(4, 2) + rows_only(8) + [(4, 2, "p2p"), (8, 1, "p2p")]
     assert grid_candidates(3, 64) == rows_only(3) + [(3, 1, "p2p")]   # odd world: rows only
-    assert grid_candidates(8, 32) == [(2, 4, "allgather"), (2, 4, "reduce"), (4, 2, "allgather"),
-                                      (4, 2, "reduce")] + rows_only(8) + [(4, 2, "p2p"), (8, 1, "p2p")]  # 4-col shares: no
+    assert grid_candidates(8, 32) == [(2, 4, "allgather")] + red(2, 4) + [(4, 2, "allgather")] + red(4, 2) + \
+        rows_only(8) + [(4, 2, "p2p"), (8, 1, "p2p")]  # 4-col shares: no 1 x 8
     assert (4, 1, "reduce") not in grid_candidates(4, 64, bipartite=False)
     for R, F, _ in grid_candidates(8, 256):
         assert R * F == 8 and (256 // F) % 4 == 0
@@ -267,19 +268,20 @@ class CpuReducePlan:
         if y is not None and mode in (_ffi.EPI_INIT, _ffi.EPI_ADD):
             y[self.own] = v
 
-    def run_item_epilogue(self, v_items, e, acc, mode, div, mul, share=False):
+    def run_pair(self, x_users, part_items, x_items, e, acc, y, mode, div, mul):
+        self.run_partial(x_users, part_items)
+        self.run_users(x_items, e, acc, y, mode, div, mul)
+
+    def finish_items(self, x0i, layers, last_share, out_i, div, mul):
         self.log.append("items")
-        if share:
-            a, b = self.share
-            rows = np.arange(a, b)
-            v = v_items[:b - a].clone()
-        else:
-            rows = np.arange(self.N - self.U)
-            v = v_items[:self.N - self.U].clone()
-        self._epi(acc[1], e[1], rows, v, mode, div, mul)
+        a, b = self.share
+        s = x0i[a:b].clone()
+        for t in list(layers) + [last_share]:
+            s = s + (t[a:b] if t is not last_share else t[:b - a])
+        out_i[a:b] = (s / div) * mul
 
 
-def _reduce_worker(rank, world, port, kind, K, out_dir, F=1):
+def _reduce_worker(rank, world, port, kind, K, out_dir, F=1, fused=False):
     import sys
 
     from conftest import PKG, ROOT
@@ -301,7 +303,7 @@ def _reduce_worker(rank, world, port, kind, K, out_dir, F=1):
     group = grid.exchange_group(dist)
     red = ItemReducer(grid.R, group)
     ou, oi = propagate_forward_reduced(torch.from_numpy(uw[:, c0:c1].copy()), torch.from_numpy(iw[:, c0:c1].copy()),
-                                       plan, K, red)
+                                       plan, K, red, fused=fused)
     ua, ub = shards.users(g)
     a, b = plan.share
     np.save(os.path.join(out_dir, f"u{g}_{grid.col_group}.npy"), ou[ua:ub].numpy())
@@ -310,13 +312,18 @@ def _reduce_worker(rank, world, port, kind, K, out_dir, F=1):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,world,K,F", [("sym", 2, 3, 1), ("sub", 2, 3, 1), ("hub", 3, 4, 1), ("sym", 4, 2, 2),
-                                            ("sub", 4, 1, 1), ("hub", 2, 3, 1), ("sub", 8, 3, 2), ("sym", 2, 0, 1)])
-def test_reduce_mode_matches_oracle(tmp_path, kind, world, K, F):
+@pytest.mark.parametrize("kind,world,K,F,fused", [("sym", 2, 3, 1, False), ("sub", 2, 3, 1, False),
+                                                  ("hub", 3, 4, 1, False), ("sym", 4, 2, 2, False),
+                                                  ("sub", 4, 1, 1, False), ("hub", 2, 3, 1, False),
+                                                  ("sub", 8, 3, 2, False), ("sym", 2, 0, 1, False),
+                                                  ("hub", 3, 4, 1, True), ("sub", 4, 1, 1, True),
+                                                  ("sub", 8, 3, 2, True)])
+def test_reduce_mode_matches_oracle(tmp_path, kind, world, K, F, fused):
     """The reduce mode (users sharded, item rows all-reduced per layer, the last layer
     reduce-scattered) over gloo: every row group's users and its share of the items within 1e-5
     per row of the one-rank oracle forward (an item row is the sum of R partial chains), the
-    shares covering every item, and the pass order of the overlapped schedule."""
+    shares covering every item, and the pass order (the item rows' stack mean once, at the end);
+    fused: the layer's two passes issued as one pair."""
     import graphs
     from oracle import lgconv_ref as R
     from parity import assert_rows_close
@@ -325,7 +332,7 @@ def test_reduce_mode_matches_oracle(tmp_path, kind, world, K, F):
 
     U, I, ei = _graph(kind)
     port = _free_port()
-    mp.spawn(_reduce_worker, args=(world, port, kind, K, str(tmp_path), F), nprocs=world, join=True)
+    mp.spawn(_reduce_worker, args=(world, port, kind, K, str(tmp_path), F, fused), nprocs=world, join=True)
     uw, iw = graphs.embeddings(U, I, 16, seed=K)
     ref = R.lightgcn_forward(uw, iw, ei, K)
     ref = np.concatenate(ref) if isinstance(ref, tuple) else ref
@@ -341,7 +348,7 @@ def test_reduce_mode_matches_oracle(tmp_path, kind, world, K, F):
     assert_rows_close(got_i, ref[U:], what="items (the row groups' shares)")
     if K:
         log = list(np.load(tmp_path / "log0.npy"))
-        expect = ["partial", "users"] + ["partial", "items", "users"] * (K - 1) + ["items"]
+        expect = ["partial", "users"] * K + ["items"]
         assert log == expect, log
 
 

@@ -2,7 +2,7 @@
 ReducePlan: users sharded, item partials all-reduced) on one GPU, per R x F grid, without the
 all_reduce (a stand-in reducer that moves nothing): the time a rank spends in its kernels per K=3
 step, next to the bytes a ring all_reduce of its item partials moves per rank.
-python tools/reduce_rank_probe.py [--grids 2x1,4x1,8x1,2x2,4x2,2x4]"""
+python tools/reduce_rank_probe.py [--grids 2x1,4x1,8x1,2x2,4x2,2x4] [--orders overlapped,fused]"""
 import argparse
 import os
 import sys
@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--grids", default="2x1,4x1,8x1,2x2,4x2,2x4")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--chunk", type=int, default=256)
+    ap.add_argument("--orders", default="overlapped,fused")
     args = ap.parse_args()
     dev = torch.device("cuda")
     g = synth.ml25m_shaped(seed=0)
@@ -56,26 +57,29 @@ def main():
         grid = ShardGrid.build(R * F, 0, d, R, F)
         c0, c1 = grid.cols
         shards = UserShards.build(deg, U, R)
-        times, moved = [], 0
+        times, moved = {o: [] for o in args.orders.split(",")}, 0
         for gr in sorted({0, R - 1}):
             rplan = ReducePlan(ei, shards, gr, c1 - c0, args.chunk)
             x0u, x0i = uw[:, c0:c1].contiguous(), iw[:, c0:c1].contiguous()
             red = NoReduce(R)
-            with torch.no_grad():
-                for _ in range(3):
-                    propagate_forward_reduced(x0u, x0i, rplan, K, red)
-                torch.cuda.synchronize()
-                red.bytes = 0
-                t = time.perf_counter()
-                for _ in range(args.steps):
-                    propagate_forward_reduced(x0u, x0i, rplan, K, red)
-                torch.cuda.synchronize()
-            times.append((time.perf_counter() - t) / args.steps * 1e3)
-            moved = red.bytes / args.steps
+            for order in times:
+                fused = order == "fused"
+                with torch.no_grad():
+                    for _ in range(3):
+                        propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)
+                    torch.cuda.synchronize()
+                    red.bytes = 0
+                    t = time.perf_counter()
+                    for _ in range(args.steps):
+                        propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)
+                    torch.cuda.synchronize()
+                times[order].append((time.perf_counter() - t) / args.steps * 1e3)
+                moved = red.bytes / args.steps
             del rplan
-        print(f"grid {R}x{F} reduce: rank compute {max(times):.3f} ms/step (row groups {sorted({0, R - 1})}: "
-              f"{', '.join(f'{t:.3f}' for t in times)}); ring all_reduce bytes per rank per step {moved / 1e6:.1f} MB",
-              flush=True)
+        for order, ts in times.items():
+            print(f"grid {R}x{F} reduce ({order}): rank compute {max(ts):.3f} ms/step (row groups "
+                  f"{sorted({0, R - 1})}: {', '.join(f'{t:.3f}' for t in ts)}); ring all_reduce bytes per rank per "
+                  f"step {moved / 1e6:.1f} MB", flush=True)
 
 
 if __name__ == "__main__":
