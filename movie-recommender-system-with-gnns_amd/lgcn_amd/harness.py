@@ -165,21 +165,30 @@ def train_epoch(model, optimizer, train_loader, device) -> tuple[float, int] | N
     fast.load_state(optimizer)
     total, total_w = None, 0
     U = model.num_users
-    try:
+    bad = object()  # a batch the fused step cannot take
+
+    def device_batches():
         for batch in train_loader:
             ei = fast.device_edge_index(batch.edge_index, device)
             st = fast.step._states.get(id(ei))
-            if st is None or st[0]() is not ei:
-                if not bipartite(ei, U):
-                    if total is None:
-                        return None
-                    raise ValueError("train(): a batch is not a bipartite user-item edge list; run with "
-                                     "LGCN_HARNESS_FUSED=0")
-            loss = fast.step.step(_Batch(ei))
+            yield bad if (st is None or st[0]() is not ei) and not bipartite(ei, U) else ei
+
+    try:
+        it = device_batches()
+        ei = next(it, None)
+        if ei is bad:
+            return None  # nothing ran: the caller runs the reference loop
+        while ei is not None:
+            nxt = next(it, None)  # one batch ahead: its user rows are caught up during this step
+            if nxt is bad:
+                raise ValueError("train(): a batch is not a bipartite user-item edge list; run with "
+                                 "LGCN_HARNESS_FUSED=0")
+            loss = fast.step.step(_Batch(ei), _Batch(nxt) if nxt is not None else None)
             w = int(ei.shape[1])
             total_w += w
             contrib = loss.detach().double() * w
             total = contrib if total is None else total + contrib
+            ei = nxt
     finally:
         if total is not None:
             fast.store_state(optimizer)

@@ -157,10 +157,10 @@ class RowLazyAdam:
                                      _ffi.stream_of(self.device)), "lgcn_row_adam")
 
     def catch_up(self, rows_a: torch.Tensor | None, keys_b: torch.Tensor | None = None, off_b: int = 0,
-                 first_b: torch.Tensor | None = None) -> None:
-        """Bring the listed rows (duplicates allowed; list b filtered by first_b) up to the completed
-        step count."""
-        self._row_adam(rows_a, keys_b, off_b, first_b, None, 0, None, 0)
+                 first_b: torch.Tensor | None = None, skip_b: torch.Tensor | None = None) -> None:
+        """Bring the listed rows (duplicates allowed; list b filtered by first_b, and by skip_b[row]
+        == 0) up to the completed step count."""
+        self._row_adam(rows_a, keys_b, off_b, first_b, skip_b, 0, None, 0)
 
     # --- the owner-sharded exchange's pieces (lgcn_amd.owner): the clip norm over every rank's rows
     def sqnorm_partials(self, keys_b: torch.Tensor, skip_b: torch.Tensor, partials: torch.Tensor) -> None:

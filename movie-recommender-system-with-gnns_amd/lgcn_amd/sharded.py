@@ -578,6 +578,14 @@ class ReducePlan:
         self.n_sub = int(sel.sum().item())
         self.scratch = {}
 
+    def item_tables(self, K: int, I_pad: int, d: int, dev) -> list:
+        """K zeroed [I_pad, d] item tables of propagate_forward_reduced, allocated once per (K, d).
+        Only the padding rows' zeros are relied on: every pass writes rows [0, I)."""
+        key = ("items", K, I_pad, d)
+        if key not in self.scratch:
+            self.scratch[key] = [torch.zeros((I_pad, d), dtype=torch.float32, device=dev) for _ in range(K)]
+        return self.scratch[key]
+
     def _part(self, direction, d):
         key = (id(direction), d)
         if direction.n_partials and key not in self.scratch:
@@ -725,8 +733,12 @@ def propagate_forward_reduced(x0u: torch.Tensor, x0i: torch.Tensor, rplan, K: in
     yu = [torch.empty((U, d), dtype=torch.float32, device=dev) for _ in range(min(2, K - 1))]
     I_pad = getattr(rplan, "I_pad", I)
     # the reduced item rows of layers 1..K-1 (read by the next user pass and by the final mean),
-    # and layer K's partials (reduce-scattered into `share`); padding rows stay zero
-    part = [torch.zeros((I_pad, d), dtype=torch.float32, device=dev) for _ in range(K)]
+    # and layer K's partials (reduce-scattered into `share`); padding rows stay zero. Every pass
+    # writes every item row (rows without a partial edge get a zero-length item), so the tables are
+    # allocated zeroed once per plan and reused (no fill kernels per step)
+    bufs = getattr(rplan, "item_tables", None)
+    part = bufs(K, I_pad, d, dev) if bufs is not None else \
+        [torch.zeros((I_pad, d), dtype=torch.float32, device=dev) for _ in range(K)]
     share = torch.empty((I_pad // max(1, reducer.R), d), dtype=torch.float32, device=dev)
     e = (x0u, x0i, U)
     acc = (out_u, out_i, U)

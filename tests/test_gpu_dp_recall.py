@@ -6,8 +6,10 @@ star: Recall@20 within +-0.002 of the reference), at BASELINE configs[0]'s size
 * Data parallel (lgcn_amd.distributed, row-sparse exchange): W disjoint parts per optimizer step,
   their gradients summed in rank order / W — so after the same epochs the model has taken W-times
   fewer, larger steps than the reference's one-part-per-step loop (reference
-  utils/train_test.py:86-101 over data/dataset_handler.py:285). Measured and printed, not held to
-  the band: at W = 8 it lands 0.0018 / 0.0032 from the reference at k = 20 / 100.
+  utils/train_test.py:86-101 over data/dataset_handler.py:285). Recall@20 is held to the north
+  star's +-0.002 (measured 0.0015-0.0018 in round 3: inside, with little margin); Recall@100 is
+  printed with its band status (0.0030-0.0032 in round 3: outside). That is why bench.py's
+  default --dp-mode for training on several GPUs is "columns", not this mode.
 * Column-sharded (lgcn_amd.train_step.ColumnGroup, SURVEY §8e's parity-preserving alternative):
   every rank steps the reference's schedule on d / W columns; one all_reduce of the triplets'
   [B, 6] dot products and norms and one all_gather of the clip norm's partials per step. Its
@@ -142,6 +144,12 @@ def test_multi_gpu_training_recall(gpu, tmp_path):
         for name, r in (("column-sharded W=8", cols8), ("fused 1 GPU", plain)):
             if abs(r["recall"][k] - ref[k]) > 0.002:
                 bad.append((name, k, r["recall"][k], ref[k]))
+        dp_d = abs(dp8["recall"][k] - ref[k])
+        if k == "20" and dp_d > 0.002:  # the north star's band is on Recall@20
+            bad.append(("data-parallel W=8", k, dp8["recall"][k], ref[k]))
+        print(f"data-parallel W=8 Recall@{k}: |d| {dp_d:.5f} "
+              f"{'inside' if dp_d <= 0.002 else 'OUTSIDE'} the +-0.002 band"
+              + (" (asserted)" if k == "20" else " (printed, not asserted: k=100 is not the north star's metric)"))
         if abs(cols8["recall"][k] - plain["recall"][k]) > 0.002:
             bad.append(("cols W=8 vs 1 GPU", k))
     assert not bad, bad
