@@ -79,8 +79,13 @@ constexpr int kStage = 512;  // staged accepted scores per wave
 // chunk get consecutive slots of the SAME XCD, so they run together and share its L2 copy of the
 // chunk's rows (the queries, not the candidates, are what differs between them).
 // At <= 170 VGPRs two waves share each SIMD, so one wave's epilogue hides under the other's MFMAs.
+// D = 256 asks for one: its two candidate buffers + staging (≈ 89 KB of LDS per workgroup) leave
+// room for one workgroup (one wave per SIMD) per CU whatever the register count.
 template <int D>
-__global__ __launch_bounds__(kBlock, 2) void k_score_filter(const float* __restrict__ Qn, int64_t Qvalid, int32_t nqg,
+constexpr int score_filter_waves() { return D >= 256 ? 1 : 2; }
+
+template <int D>
+__global__ __launch_bounds__(kBlock, score_filter_waves<D>()) void k_score_filter(const float* __restrict__ Qn, int64_t Qvalid, int32_t nqg,
                                                             int32_t nchunk, const float* __restrict__ Cn, int64_t M,
                                                             int64_t stride, const uint32_t* __restrict__ thr,
                                                             uint32_t* __restrict__ list_key,

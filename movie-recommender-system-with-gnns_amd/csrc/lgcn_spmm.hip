@@ -379,13 +379,41 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
 // [0, blocks_a) run pass a, the rest pass b. Each pass keeps its own longest-first order, and b's
 // longest items start while a's last workgroups drain, so the pair pays one launch gap and one
 // drain instead of two. Per row the arithmetic is the single pass's (bitwise).
+// split_xcd: workgroups are dealt to the 8 XCDs round-robin (workgroup i on XCD i % 8), so while
+// both passes have blocks left, pass a takes the slots of XCDs 0-3 and pass b those of XCDs 4-7 —
+// each XCD's L2 then holds one pass's gather table instead of both — and the longer pass's
+// remaining blocks follow on every XCD.
 template <int LPR, int NV, int UNROLL, int TAIL, int CM>
-__global__ __launch_bounds__(kBlock) void k_spmm_pair(SpmmArgs a, SpmmArgs b, int64_t blocks_a) {
+__global__ __launch_bounds__(kBlock) void k_spmm_pair(SpmmArgs a, SpmmArgs b, int64_t blocks_a, int64_t blocks_b,
+                                                      int split_xcd) {
     const int64_t blk = blockIdx.x;
+    if (split_xcd) {
+        const int64_t m = (blocks_a < blocks_b ? blocks_a : blocks_b) & ~int64_t(3);  // 4 per round each
+        if (blk < 2 * m) {
+            const int64_t k = blk >> 3, x = blk & 7;
+            if (x < 4)
+                item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(a, k * 4 + x);
+            else
+                item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(b, k * 4 + x - 4);
+            return;
+        }
+        const int64_t r = blk - 2 * m;  // the rest of both, a's first
+        if (r < blocks_a - m)
+            item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(a, m + r);
+        else
+            item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(b, m + r - (blocks_a - m));
+        return;
+    }
     if (blk < blocks_a)
         item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(a, blk);
     else
         item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(b, blk - blocks_a);
+}
+
+// LGCN_PAIR_XCD=1: lgcn_spmm_pair's XCD-split block mapping (A/B knob; default off)
+int pair_split_xcd() {
+    const char* v = std::getenv("LGCN_PAIR_XCD");
+    return v ? std::atoi(v) : 0;
 }
 
 // Split rows: one workgroup per split row. Running sum v (of kVSums, owned by lane group v % GPB)
@@ -537,7 +565,8 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass, const SpmmArgs* b = n
         if (pass & PASS_ITEMS) {
             const int64_t ba = (a.n_items + GPB - 1) / GPB, bb = (b->n_items + GPB - 1) / GPB;
             if (ba + bb > 0) {
-                k_spmm_pair<LPR, NV, UNROLL, TAIL, CM><<<dim3(static_cast<unsigned>(ba + bb)), kBlock, 0, s>>>(a, *b, ba);
+                k_spmm_pair<LPR, NV, UNROLL, TAIL, CM><<<dim3(static_cast<unsigned>(ba + bb)), kBlock, 0, s>>>(
+                    a, *b, ba, bb, pair_split_xcd());
                 if (int rc = check_launch("k_spmm_pair")) return rc;
             }
         }

@@ -40,10 +40,13 @@ def _pass(direction, x, y, acc, part, mode, e=None, div=1.0, mul=1.0):
 
 
 @pytest.mark.parametrize("d", [4, 8, 16, 32, 64, 128, 256, 512])
-@pytest.mark.parametrize("chunk", [8, 4096])
-def test_spmm_pair_bitwise_single_passes(gpu, d, chunk):
+@pytest.mark.parametrize("chunk,xcd", [(8, "0"), (4096, "0"), (8, "1"), (4096, "1")])
+def test_spmm_pair_bitwise_single_passes(gpu, monkeypatch, d, chunk, xcd):
+    """xcd = LGCN_PAIR_XCD: the XCD-split block mapping (each pass on half the XCDs while both have
+    blocks left) gives the same rows."""
     import graphs
 
+    monkeypatch.setenv("LGCN_PAIR_XCD", xcd)
     from lgcn_amd import _ffi
     from lgcn_amd.propagate import spmm
 

@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--grids", default="2x1,4x1,8x1,2x2,4x2,2x4")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--chunk", type=int, default=256)
-    ap.add_argument("--orders", default="overlapped,fused")
+    ap.add_argument("--orders", default="overlapped,fused,fusedx")
     args = ap.parse_args()
     dev = torch.device("cuda")
     g = synth.ml25m_shaped(seed=0)
@@ -63,7 +63,9 @@ def main():
             x0u, x0i = uw[:, c0:c1].contiguous(), iw[:, c0:c1].contiguous()
             red = NoReduce(R)
             for order in times:
-                fused = order == "fused"
+                fused = order.startswith("fused")
+                # fusedx: the pair launch's XCD-split block mapping (LGCN_PAIR_XCD=1)
+                os.environ["LGCN_PAIR_XCD"] = "1" if order == "fusedx" else "0"
                 with torch.no_grad():
                     for _ in range(3):
                         propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)
