@@ -115,7 +115,10 @@ int lgcn_csr_build(const int64_t* key, const int64_t* other, int64_t E, int64_t 
  * ascending order. cursor: device int32[lgcn_group_keys_cursor_len(R)] scratch whose first R
  * entries are zero on entry (allocate it zeroed) and are left zero on exit — no memset, so the
  * call captures into a hipGraph as kernels only (the tail holds per-tile totals).
- * Meant for many keys over a small range with
+ * Integrity: the kernels check every index they write through (the counts must add up to B,
+ * placements and groups must lie inside perm[0, B)); a failed check adds 2^32 to *err_count and
+ * drops the write instead of faulting — so *err_count >= 2^32 means the grouping is invalid
+ * (below 2^32 it counts out-of-range keys). Meant for many keys over a small range with
  * short groups (the per-step negatives, B ~ 1.8e5 over I = 59,047 items: ~3 per key); a group's
  * ordering is quadratic in its length. B < 2^31, R < 2^31.
  * Replaces: the per-step grouping that index_put_(accumulate) performs implicitly in the

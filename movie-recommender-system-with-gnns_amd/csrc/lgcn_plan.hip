@@ -443,7 +443,8 @@ __global__ __launch_bounds__(kScanTile) void k_group_tile_sums(const int32_t* __
 
 __global__ __launch_bounds__(kScanTile) void k_group_scan(int32_t* __restrict__ count_cursor, int64_t R,
                                                           const int32_t* __restrict__ tsum,
-                                                          int64_t* __restrict__ rowptr) {
+                                                          int64_t* __restrict__ rowptr, int64_t B,
+                                                          unsigned long long* __restrict__ err) {
     using Scan = hipcub::BlockScan<int32_t, kScanTile>;
     using Reduce = hipcub::BlockReduce<int32_t, kScanTile>;
     __shared__ typename Scan::TempStorage tmp;
@@ -464,7 +465,12 @@ __global__ __launch_bounds__(kScanTile) void k_group_scan(int32_t* __restrict__ 
         rowptr[i] = run;
         count_cursor[i] = run;
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) rowptr[R] = s_off + total;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        rowptr[R] = s_off + total;
+        // the counts must add up to the B keys: anything else means the count array was not zero
+        // on entry (the cursor contract broken), and every later index would be off
+        if (s_off + total != B) atomicAdd(err, 1ull << 32);
+    }
 }
 
 __global__ void k_group_place(const int64_t* __restrict__ key, int64_t B, int64_t R,
@@ -475,8 +481,9 @@ __global__ void k_group_place(const int64_t* __restrict__ key, int64_t B, int64_
         bool bad;
         const int64_t k = group_key(key, b, R, bad);
         const int32_t pos = atomicAdd(&cursor[k], 1);
-        if (pos < rowptr[k] || pos >= rowptr[k + 1]) {  // cannot happen when count and key agree
-            atomicAdd(err, 1ull);
+        // cannot happen when count and key agree; pos < B also holds a corrupted rowptr to perm's size
+        if (pos < rowptr[k] || pos >= rowptr[k + 1] || pos >= B) {
+            atomicAdd(err, 1ull << 32);
             continue;
         }
         perm[pos] = static_cast<int32_t>(b);
@@ -486,11 +493,15 @@ __global__ void k_group_place(const int64_t* __restrict__ key, int64_t B, int64_
 // Each key's positions in ascending order (insertion sort; groups are a few entries long); the
 // cursor is zeroed for the next call (no memset node in a captured step).
 __global__ void k_group_order(const int64_t* __restrict__ rowptr, int64_t R, int32_t* __restrict__ perm,
-                              int32_t* __restrict__ cursor) {
+                              int32_t* __restrict__ cursor, int64_t B, unsigned long long* __restrict__ err) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < R; r += stride) {
         cursor[r] = 0;
         const int64_t beg = rowptr[r], end = rowptr[r + 1];
+        if (beg < 0 || end < beg || end > B) {  // a corrupted rowptr: count it, write nothing
+            atomicAdd(err, 1ull << 32);
+            continue;
+        }
         for (int64_t i = beg + 1; i < end; ++i) {
             const int32_t v = perm[i];
             int64_t j = i - 1;
@@ -578,13 +589,13 @@ int lgcn_group_keys(const int64_t* key, int64_t B, int64_t R, int64_t* rowptr, i
     int32_t* tsum = cursor + R;  // the tail of the caller's scratch: one total per tile
     k_group_tile_sums<<<static_cast<unsigned>(tiles), kScanTile, 0, s>>>(cursor, R, tsum);
     if (int rc = check_launch("k_group_tile_sums")) return rc;
-    k_group_scan<<<static_cast<unsigned>(tiles), kScanTile, 0, s>>>(cursor, R, tsum, rowptr);
+    k_group_scan<<<static_cast<unsigned>(tiles), kScanTile, 0, s>>>(cursor, R, tsum, rowptr, B, err);
     if (int rc = check_launch("k_group_scan")) return rc;
     if (B > 0) {
         k_group_place<<<grid_for(B, kBlock, 4096), kBlock, 0, s>>>(key, B, R, rowptr, cursor, perm, err);
         if (int rc = check_launch("k_group_place")) return rc;
     }
-    k_group_order<<<grid_for(R, kBlock, 4096), kBlock, 0, s>>>(rowptr, R, perm, cursor);
+    k_group_order<<<grid_for(R, kBlock, 4096), kBlock, 0, s>>>(rowptr, R, perm, cursor, B, err);
     return check_launch("k_group_order");
 }
 

@@ -84,7 +84,13 @@ class _Fast:
         self.lr = float(g["lr"])
         uw, iw = model.user_embedding.weight, model.item_embedding.weight
         self.opt = RowLazyAdam(uw.data, iw.data, lr=self.lr, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=1.0)
-        self.step = FusedTrainStep(model, self.opt, lazy=True, graphs=True)
+        from utils import helpers
+
+        num_items, dev = model.num_items, uw.device
+        # the negatives come from the harness's own sampler (reference utils/helpers.py:64-82):
+        # the reference loop's draws, and whatever a caller substitutes for them
+        self.step = FusedTrainStep(model, self.opt, lazy=True, graphs=True,
+                                   neg_sampler=lambda pos: helpers.sample_negative(pos, num_items, dev))
         # device copies of the loader's batches (keyed by the host edge_index, held weakly), so a
         # batch keeps its plans and captured graph from epoch to epoch
         self.dev_batches: dict[int, tuple[weakref.ref, torch.Tensor]] = {}

@@ -319,7 +319,7 @@ class FusedTrainStep:
 
     def __init__(self, model, optimizer, bpr_coeff: float = 5e-3, world: int = 1, max_entries: int = 4096,
                  graphs: bool = False, lazy: bool = False, exchange=None, neg_seed: int | None = None,
-                 cols: ColumnGroup | None = None):
+                 cols: ColumnGroup | None = None, neg_sampler=None):
         """graphs=True: the first step of each batch runs eagerly, then the whole step (gradients
         and, at world == 1, the optimizer — which must be a capturable FusedAdam) is captured in a
         per-batch hipGraph and replayed from then on; negatives still come from the global CUDA
@@ -332,7 +332,10 @@ class FusedTrainStep:
         global CUDA generator (the same draws whichever exchange runs, and whenever they are drawn).
         cols (lazy): column-sharded training — the model holds this rank's ColumnGroup columns,
         every rank steps the same batches with the same negatives (the same neg_seed); with graphs,
-        each batch's step is captured as graphs cut at the two collectives (_SegmentedGraph)."""
+        each batch's step is captured as graphs cut at the two collectives (_SegmentedGraph).
+        neg_sampler (pos_items [B] -> item ids [B]): draw the negatives with it (the harness passes
+        utils.helpers.sample_negative, so what that function draws — patched or not — is what the
+        step trains on); default: torch.randint(0, I, (B,)) into the batch's buffer, the same draws."""
         self.model = model
         self.optimizer = optimizer
         self.coeff = float(bpr_coeff)
@@ -363,6 +366,7 @@ class FusedTrainStep:
         if self.owner and not lazy:
             raise ValueError("an OwnerExchange needs lazy=True (RowLazyAdam)")
         self.neg_seed = neg_seed
+        self.neg_sampler = neg_sampler
         self._gen = None
         self._k = 0  # steps taken (the index of the next step)
         self._owner_graphs = None
@@ -389,6 +393,10 @@ class FusedTrainStep:
         m = self.model
         dev = m.user_embedding.weight.device
         k = self._k if k is None else k
+        if self.neg_sampler is not None:
+            st.neg.copy_(self.neg_sampler(st.pos))
+            st.neg_step = k
+            return
         gen = None
         if self.neg_seed is not None:
             if self._gen is None:
@@ -698,6 +706,9 @@ class FusedTrainStep:
         for ref, _, st in self._states.values():
             if getattr(st, "overflow", None) is not None and int(st.overflow.item()):
                 raise RuntimeError("lgcn_range_scatter_add overflowed: negatives too concentrated for its lists")
+            if getattr(st, "neg_err", None) is not None and int(st.neg_err.item()):
+                # the grouping's integrity checks (lgcn_group_keys: >= 2^32) or an out-of-range key
+                raise RuntimeError(f"negatives grouping reported errors ({int(st.neg_err.item()):#x})")
 
     def _optimize(self) -> None:
         if getattr(self.optimizer, "fused_clip_norm", None) is None:

@@ -3,9 +3,11 @@ reference-style loop (autograd + torch Adam + clip_grad_norm_, LGCN_HARNESS_FUSE
 batch step it routes to by default (lgcn_amd.harness: HIP forward / BPR / backward, exact row-lazy
 Adam, one hipGraph per batch). Same model init, same seed, so the same negatives: the epoch loss
 within 1e-5, and after every epoch the tables and Adam moments within 1e-5 per row on the elements
-whose gradient is settled (clear of the 1e-5 gradient bar by 10x in every step: Adam's early steps
-move a weight by about lr * sign(grad), so a noise-level gradient's sign is not a parity statement;
-those elements are counted and printed), the rows that move identical, the step counts equal.
+whose Adam steps are well conditioned (_settled: every step's gradient clear of the per-row
+gradient bar by 10x, and the first moment not a near-cancellation of earlier gradients, which
+would amplify the gradients' 1e-6-level summation-order differences; those elements are counted
+and printed), the second moments within 1e-5 per row everywhere, the
+rows that move identical, the step counts equal.
 Epoch 2 starts from the torch optimizer state epoch 1 wrote back (the paths can alternate)."""
 import numpy as np
 import pytest
@@ -58,6 +60,30 @@ def _run(gpu, monkeypatch, fused, U, I, d, init, loader, epochs=2):
     return out, grads
 
 
+def _settled(grads, frac=0.05):
+    """Per table, the elements whose Adam update is well conditioned in every step: the first
+    moment m_s (the reference's clipped gradients, beta1 = 0.9) is at least `frac` of the same
+    average taken over |g|. Where it is smaller, m is a near-cancellation of earlier steps'
+    gradients and its relative error — hence the step's, hence the weight's — is the gradients'
+    1e-6-level summation-order differences amplified by that factor; those elements are counted,
+    not held to the bar. (One step: m = 0.1 g, every nonzero gradient element is settled.)"""
+    m = [np.zeros(g.shape, np.float64) for g in grads[0]]
+    a = [np.zeros(g.shape, np.float64) for g in grads[0]]
+    ok = [np.ones(g.shape, bool) for g in grads[0]]
+    for gs in grads:
+        gn = [g.double().cpu().numpy() for g in gs]
+        norm = np.sqrt(sum(float((g * g).sum()) for g in gn))
+        c = min(1.0, 1.0 / (norm + 1e-6))
+        for t, g in enumerate(gn):
+            m[t] = 0.9 * m[t] + 0.1 * c * g
+            a[t] = 0.9 * a[t] + 0.1 * c * np.abs(g)
+            ok[t] &= np.abs(m[t]) >= frac * a[t]
+            # and each step's gradient clear of the per-row 1e-5 gradient bar by 10x (or exactly 0):
+            # a noise-level gradient's relative error is its own, not the row's
+            ok[t] &= (g == 0) | (np.abs(g) > 1e-4 * np.abs(g).max(axis=1, keepdims=True))
+    return ok
+
+
 def _compare(ref, got, grads, w0, what):
     from parity import assert_rows_close
 
@@ -68,11 +94,9 @@ def _compare(ref, got, grads, w0, what):
         assert g["step"] == r["step"], (g["step"], r["step"])
         n_steps = int(r["step"][0])
         stats = {}
+        masks = _settled(grads[:n_steps])
         for t, name in enumerate(("user", "item")):
-            gs = [s[t].cpu().numpy() for s in grads[:n_steps]]
-            settled = np.ones_like(gs[0], dtype=bool)
-            for gt in gs:
-                settled &= (gt == 0) | (np.abs(gt) > 1e-4 * np.abs(gt).max(axis=1, keepdims=True))
+            settled = masks[t]
             # the same rows move
             assert np.array_equal(np.any(g["w"][t] != w0[t], axis=1), np.any(r["w"][t] != w0[t], axis=1)), name
             for key in ("w", "m"):

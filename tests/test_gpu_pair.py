@@ -105,13 +105,13 @@ def test_stack_mean_rows_bitwise_epilogues(gpu, K):
     ys = [torch.randn(rows, d, device=gpu, generator=g) * 10 ** (-k) for k in range(K)]
     div = float(K + 1)
     mul = float(np.float32(1.0 / (K + 1)))
-    if K == 1:
-        ref = ((e + ys[0]) / div) * mul
-    else:
-        acc = e + ys[0]
-        for y in ys[1:-1]:
-            acc = acc + y
-        ref = ((acc + ys[-1]) / div) * mul
+    # numpy fp32: one correctly rounded op at a time (torch's CUDA `tensor / scalar` multiplies by
+    # the scalar's reciprocal instead, which is not the epilogue's division)
+    en, yn = e.cpu().numpy(), [y.cpu().numpy() for y in ys]
+    acc = en + yn[0]
+    for y in yn[1:]:
+        acc = acc + y
+    ref = torch.from_numpy((acc / np.float32(div)) * np.float32(mul)).to(gpu)
     out = torch.empty_like(e)
     arr = (ctypes.c_void_p * K)(*[y.data_ptr() for y in ys])
     lib = _ffi.load()

@@ -301,6 +301,32 @@ def test_group_keys_out_of_range_keys(gpu):
     np.testing.assert_array_equal(pm_g, pm_c)
 
 
+def test_group_keys_detects_a_dirty_cursor(gpu):
+    """Round 2's captured-step fault needed counts that were not zero on entry (the memset node did
+    not account for it: tests/test_gpu_memset_capture.py). The grouping now checks what a dirty
+    count array breaks — the counts' total against B, every placement and every group against
+    perm[0, B) — reports it as err >= 2^32 and writes nothing outside perm (a guard region after it
+    stays intact), instead of writing out of bounds."""
+    from lgcn_amd import _ffi
+
+    lib = _ffi.load()
+    s = _ffi.stream_of(gpu)
+    B, R, guard = 20000, 5000, 4096
+    keys = torch.from_numpy(np.random.default_rng(1).integers(0, R, B).astype(np.int64)).to(gpu)
+    rowptr = torch.empty(R + 1, dtype=torch.int64, device=gpu)
+    buf = torch.full((B + guard,), -7, dtype=torch.int32, device=gpu)
+    perm = buf[:B]
+    err = torch.zeros(1, dtype=torch.int64, device=gpu)
+    cursor = torch.zeros(int(lib.lgcn_group_keys_cursor_len(R)), dtype=torch.int32, device=gpu)
+    cursor[:R] = 50  # what a skipped reset would leave: large counts everywhere
+    _ffi.check(lib.lgcn_group_keys(keys.data_ptr(), B, R, rowptr.data_ptr(), perm.data_ptr(), cursor.data_ptr(),
+                                   err.data_ptr(), s), "lgcn_group_keys")
+    torch.cuda.synchronize()
+    assert int(err.item()) >= 1 << 32
+    assert bool((buf[B:] == -7).all().item())
+    assert int(cursor[:R].abs().sum().item()) == 0  # left zero for the next call all the same
+
+
 @pytest.mark.parametrize("B,nrows,d", [(3000, 500, 64), (20000, 59047, 128), (5000, 40, 32), (180000, 59047, 128)])
 def test_sorted_no_parking_plus_grouped_reg_equals_parked(gpu, B, nrows, d):
     """The sorted path without the parking table (lgcn_sorted_scatter_add with no second source:
