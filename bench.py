@@ -414,8 +414,6 @@ def main():
                          "row-lazy Adam (all_gather of every rank's gradient rows) or an owner-sharded one (two "
                          "all_to_alls) — W-times fewer, larger Adam steps: Recall@20 within the +-0.002 band "
                          "with little margin at W = 8, Recall@100 outside it (tests/test_gpu_dp_recall.py)")
-    ap.add_argument("--no-prefetch", action="store_true",
-                    help="train, N=1: do not catch the next batch's user rows up beside each step")
     ap.add_argument("--no-harness", action="store_true",
                     help="train, N=1: skip timing utils.train_test.train() both ways after the bench line's run")
     ap.add_argument("--dense-adam", action="store_true",
@@ -889,8 +887,7 @@ def run_train(args):
     def step(bidx, nxt=None):
         batch = batches[bidx]
         if fused is not None:
-            if dp_mode == "owner" or (world == 1 and not args.no_prefetch):
-                # owner: the next step's rows are fetched; one GPU: its user rows caught up meanwhile
+            if dp_mode == "owner":
                 fused.step(batch, batches[nxt] if nxt is not None else None)
             else:
                 fused.step(batch)
@@ -909,9 +906,8 @@ def run_train(args):
              D.rank_share(len(batches), world, rank, seed=0, epoch=0))
 
     def nxt_of(i, last):
-        """the batch index of step i + 1 (owner mode fetches its rows; one GPU catches its user rows
-        up beside step i), None after an epoch's end (sync() makes every row current there) or the
-        run's last step"""
+        """the batch index of step i + 1 (owner mode fetches its rows), None after an epoch's end
+        (sync() makes every row current there) or the run's last step"""
         return None if (i + 1) % len(share) == 0 or i + 1 == last else share[(i + 1) % len(share)]
 
     n_warm = max(args.warmup, 2 * len(share))

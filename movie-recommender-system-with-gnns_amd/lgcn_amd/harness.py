@@ -185,11 +185,11 @@ def train_epoch(model, optimizer, train_loader, device) -> tuple[float, int] | N
         if ei is bad:
             return None  # nothing ran: the caller runs the reference loop
         while ei is not None:
-            nxt = next(it, None)  # one batch ahead: its user rows are caught up during this step
+            nxt = next(it, None)
             if nxt is bad:
                 raise ValueError("train(): a batch is not a bipartite user-item edge list; run with "
                                  "LGCN_HARNESS_FUSED=0")
-            loss = fast.step.step(_Batch(ei), _Batch(nxt) if nxt is not None else None)
+            loss = fast.step.step(_Batch(ei))
             w = int(ei.shape[1])
             total_w += w
             contrib = loss.detach().double() * w

@@ -174,9 +174,6 @@ class _BatchState:
             self.fixed_dense, self.fixed_sparse, self.fixed_touched = segment_directions(
                 self.keys[:2 * B], N, chunk=32, row_mask=self.plan.touched)
             self.touched_rows = torch.nonzero(self.plan.touched).squeeze(1).to(torch.int32).contiguous()
-            # the touched USER rows (ascending ids: a prefix of touched_rows), int64 for the row Adam's
-            # filtered list: what the previous step catches up ahead of this one (FusedTrainStep.step)
-            self.touched_users = self.touched_rows[self.touched_rows < U].to(torch.int64).contiguous()
         elif self.small:
             self.fixed_dense, self.fixed_sparse = segment_directions(self.keys[:2 * B], N, chunk=32)
         if self.small and B >= sorted_scatter_min_b():
@@ -694,7 +691,6 @@ class FusedTrainStep:
             self._synced = True
             return
         if self.lazy:
-            self._await_prefetch()  # the flush replays every row: no side catch-up may be in flight
             self.optimizer.flush()
 
     def check_overflow(self) -> None:
@@ -721,56 +717,17 @@ class FusedTrainStep:
         allreduce_grads([self.model.user_embedding.weight, self.model.item_embedding.weight], self.world)
 
     def step(self, batch, next_batch=None) -> torch.Tensor:
-        """One training step on batch. next_batch (the batch the NEXT step will take): owner-sharded
-        — its rows are fetched from their owners at the end of this step; one GPU, row-lazy — its
-        user rows are caught up on a side stream while this step runs (_prefetch_users)."""
+        """One training step on batch. next_batch (owner-sharded: the batch the NEXT step will
+        take): its rows are fetched from their owners at the end of this step."""
         if self.owner:
             st = self.state(batch.edge_index)
             nxt = self.state(next_batch.edge_index) if next_batch is not None else None
             if not st.lazy or (nxt is not None and not nxt.lazy):
                 raise ValueError("lazy step needs a batch whose 3B contribution ids fit int32 (3B < 2^31)")
             return self._step_owner(st, nxt)
-        self._await_prefetch()  # a catch-up issued ahead of this step has landed before it reads rows
-        if self._prefetching(next_batch):
-            self._prefetch_users(self.state(batch.edge_index), self.state(next_batch.edge_index))
         loss = self._step_replicated(batch)
         self._k += 1
         return loss
-
-    # --- one GPU: the next batch's user rows caught up while this step runs ----------------------
-    # A Cluster-GCN batch's touched user rows belong to its parts alone, and negatives are items, so
-    # no other batch's step writes them; their catch-up (the replay of ~one epoch of zero-gradient
-    # Adam steps, most of the catch-up launch's work) can run on a side stream beside the previous
-    # step. Rows the running step does touch are skipped on the device (skip_b = its touched mask),
-    # so any next_batch is safe; the side kernel reads the step counter before or after the
-    # running step's update advances it — either way a row outside that update's list replays to a
-    # step it was never updated in, which is exact — and the next step's own catch-up finishes
-    # whatever is left (at most one step per row).
-    def _prefetching(self, next_batch) -> bool:
-        return (next_batch is not None and self.lazy and self.exchange is None and self.cols is None
-                and self.world == 1)
-
-    def _prefetch_users(self, st, nst) -> None:
-        if not nst.lazy or nst is st or nst.touched_users.numel() == 0:
-            return
-        dev = self.model.user_embedding.weight.device
-        main = torch.cuda.current_stream(dev)
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(dev)
-        start = torch.cuda.Event()
-        start.record(main)
-        with torch.cuda.stream(self._side):
-            self._side.wait_event(start)
-            self.optimizer.catch_up(None, nst.touched_users, 0, skip_b=st.plan.touched)
-            done = torch.cuda.Event()
-            done.record(self._side)
-        self._pf_event = done
-
-    def _await_prefetch(self) -> None:
-        ev = getattr(self, "_pf_event", None)
-        if ev is not None:
-            torch.cuda.current_stream(self.model.user_embedding.weight.device).wait_event(ev)
-            self._pf_event = None
 
     def _step_replicated(self, batch) -> torch.Tensor:
         if self.lazy:

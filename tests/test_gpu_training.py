@@ -492,44 +492,3 @@ def test_planted_shape_captured_step_bitwise_range_path(gpu, monkeypatch, lazy):
         assert other[0] == res[0][0]
         assert torch.equal(other[1], res[0][1]) and torch.equal(other[2], res[0][2])
 
-
-@pytest.mark.parametrize("use_graphs,clip", [(False, 1.0), (True, 1.0), (True, None)])
-def test_next_batch_user_prefetch_is_bitwise(gpu, use_graphs, clip):
-    """FusedTrainStep.step(batch, next_batch) catches the next batch's user rows up on a side stream
-    while the step runs: every loss and both tables bitwise the same steps without it, over three
-    epochs of Cluster-GCN batches (in a shuffled order per epoch, a repeated batch included: the
-    running step's own rows are skipped on the device), with the epoch-end sync() in between."""
-    from lgcn_amd import cluster as C
-    from lgcn_amd.optim import RowLazyAdam
-    from lgcn_amd.train_step import FusedTrainStep
-    from models.light_gcn import LightGCN
-
-    import graphs
-
-    U, I, ei = graphs.subsampled(U=2000, I=1000, pairs=8000, seed=4)
-    part = C.partition_nodes(ei, U + I, 8)
-    batches = [_Batch(torch.from_numpy(x).to(gpu)) for x in C.intra_part_edges(ei, part, 8)]
-    rng = np.random.default_rng(3)
-    order = [list(rng.permutation(8)) for _ in range(3)]
-    order[1][3] = order[1][2]  # the same batch twice in a row: the prefetch must skip its own rows
-    res = []
-    for prefetch in (False, True):
-        torch.manual_seed(0)
-        m = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
-        opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-2, max_grad_norm=clip)
-        step = FusedTrainStep(m, opt, graphs=use_graphs, lazy=True)
-        losses = []
-        for ep in order:
-            for j, b in enumerate(ep):
-                torch.cuda.manual_seed(100 + len(losses))
-                nxt = batches[ep[j + 1]] if prefetch and j + 1 < len(ep) else None
-                losses.append(step.step(batches[b], nxt).item())
-            step.sync()
-        res.append((losses, m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone(),
-                    [t.clone() for t in (*opt.m, *opt.v)], opt.last.clone()))
-    assert res[0][0] == res[1][0]
-    for a, b in zip(res[0][1:3], res[1][1:3]):
-        assert torch.equal(a, b)
-    for a, b in zip(res[0][3], res[1][3]):
-        assert torch.equal(a, b)
-    assert torch.equal(res[0][4], res[1][4])
