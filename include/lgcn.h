@@ -268,7 +268,10 @@ int lgcn_spmm_blocksplit(const lgcn_item_t* items, int64_t n_items, const lgcn_s
  * lgcn_spmm_combine give for each pass alone; the two passes must not write what the other reads.
  * The reduce-mode sharded forward (lgcn_amd/sharded.py) pairs a layer's user pass (users from the
  * item table) with its item-partial pass (items from the rank's users): one launch gap and one
- * drain per pair instead of two. Vector widths only (d in {4, 8, ..., 1024}, 16-byte aligned rows).
+ * drain per pair instead of two. While both passes have workgroups left, pass a takes the slots the
+ * round-robin dispatch deals to XCDs 0-3 and pass b those of XCDs 4-7, so each XCD's L2 caches
+ * one pass's gather table (env LGCN_PAIR_XCD=0: a's workgroups, then b's, on every XCD).
+ * Vector widths only (d in {4, 8, ..., 1024}, 16-byte aligned rows).
  * Replaces, like lgcn_spmm, LGConv.forward at reference models/light_gcn.py:33 (ABI 5). */
 typedef struct {
     const lgcn_item_t* items;
@@ -291,6 +294,11 @@ typedef struct {
     int32_t mode;
     float div;
     float mul;
+    /* combine layout: -1 = every split row gets a workgroup (lgcn_spmm's combine); n >= 0 = split
+     * rows [0, n) may have any chunk count, rows [n, n_splits) have at most 16 chunks (pcnt <= 16)
+     * and are combined one per lane group instead — the same association, so the same bits, with
+     * a fraction of the workgroups (a rank plan has thousands of 2-16-chunk split rows) */
+    int64_t n_split_big;
 } lgcn_pass_t;
 int lgcn_spmm_pair(const lgcn_pass_t* a, const lgcn_pass_t* b, int64_t N, int32_t d, int32_t what,
                    lgcn_stream_t stream);

@@ -54,6 +54,9 @@ struct SpmmArgs {
     float* run;  // sliced launches: running row sums between a row's source-slice segments
     const lgcn_item_t* chunks;  // block-split launches: split rows' chunk items, partial-slot order
     int32_t nt = 0;  // bit 0: non-temporal row stores, bit 1: non-temporal row loads (LGCN_SPMM_NT overrides)
+    // combine launches: split rows [0, n_big) get a workgroup each; rows [n_big, n_splits) have at
+    // most kVSums chunks and are combined one per lane group (lgcn_spmm_pair's n_split_big)
+    int64_t n_big = -1;  // -1: every split row gets a workgroup
 };
 
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
 // [0, blocks_a) run pass a, the rest pass b. Each pass keeps its own longest-first order, and b's
 // longest items start while a's last workgroups drain, so the pair pays one launch gap and one
 // drain instead of two. Per row the arithmetic is the single pass's (bitwise).
-// split_xcd: workgroups are dealt to the 8 XCDs round-robin (workgroup i on XCD i % 8), so while
+// split_xcd (the default): workgroups are dealt to the 8 XCDs round-robin (workgroup i on XCD i % 8), so while
 // both passes have blocks left, pass a takes the slots of XCDs 0-3 and pass b those of XCDs 4-7 —
 // each XCD's L2 then holds one pass's gather table instead of both — and the longer pass's
 // remaining blocks follow on every XCD.
@@ -410,10 +413,11 @@ __global__ __launch_bounds__(kBlock) void k_spmm_pair(SpmmArgs a, SpmmArgs b, in
         item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(b, blk - blocks_a);
 }
 
-// LGCN_PAIR_XCD=1: lgcn_spmm_pair's XCD-split block mapping (A/B knob; default off)
+// lgcn_spmm_pair's XCD-split block mapping: on by default (reduce-mode 4 x 2 rank step, K=3, C2:
+// 0.193 -> 0.176 ms; 8 x 1 0.182 vs 0.184, profiles/r04a_pair/); LGCN_PAIR_XCD=0 turns it off.
 int pair_split_xcd() {
     const char* v = std::getenv("LGCN_PAIR_XCD");
-    return v ? std::atoi(v) : 0;
+    return v ? std::atoi(v) : 1;
 }
 
 // Split rows: one workgroup per split row. Running sum v (of kVSums, owned by lane group v % GPB)
@@ -474,14 +478,52 @@ __global__ __launch_bounds__(kBlock) void k_combine_vec(SpmmArgs a) {
     combine_row<LPR, NV>(a, blockIdx.x);
 }
 
-// The split rows of two passes in one launch: workgroups [0, a.n_splits) combine a's, the rest b's.
+// A split row of at most kVSums chunks, combined by one lane group: running sum v holds partial v
+// alone (0 + p_v), and the sums are added in v order — combine_row's association for such a row,
+// so bitwise its result — without a workgroup, LDS or a barrier per row.
 template <int LPR, int NV>
-__global__ __launch_bounds__(kBlock) void k_combine_pair(SpmmArgs a, SpmmArgs b) {
-    const int64_t s = blockIdx.x;
-    if (s < a.n_splits)
-        combine_row<LPR, NV>(a, s);
+__device__ __forceinline__ void combine_small_row(const SpmmArgs& a, int64_t s, int l) {
+    const lgcn_split_t sp = a.splits[s];
+    const int64_t d4 = int64_t(LPR) * NV;
+    const float4* p = reinterpret_cast<const float4*>(a.partial) + int64_t(sp.pbeg) * d4 + l;
+    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = f4_add(zero, p[k * LPR]);
+    for (int c = 1; c < sp.pcnt; ++c)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], f4_add(zero, p[int64_t(c) * d4 + k * LPR]));
+    finish_row_vec<LPR, NV>(a, sp.row, l, acc);
+}
+
+// Workgroups of one pass's combine: a.n_big whole-workgroup rows, then the small rows GPB per block.
+template <int LPR, int NV>
+__host__ __device__ __forceinline__ int64_t combine_blocks(const SpmmArgs& a) {
+    constexpr int GPB = kBlock / LPR;
+    const int64_t big = a.n_big < 0 ? a.n_splits : a.n_big;
+    return big + (a.n_splits - big + GPB - 1) / GPB;
+}
+
+template <int LPR, int NV>
+__device__ __forceinline__ void combine_block(const SpmmArgs& a, int64_t blk) {
+    constexpr int GPB = kBlock / LPR;
+    const int64_t big = a.n_big < 0 ? a.n_splits : a.n_big;
+    if (blk < big) {
+        combine_row<LPR, NV>(a, blk);
+        return;
+    }
+    const int64_t s = big + (blk - big) * GPB + threadIdx.x / LPR;
+    if (s < a.n_splits) combine_small_row<LPR, NV>(a, s, threadIdx.x % LPR);
+}
+
+// The split rows of two passes in one launch: a's workgroups first, then b's.
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_combine_pair(SpmmArgs a, SpmmArgs b, int64_t blocks_a) {
+    const int64_t blk = blockIdx.x;
+    if (blk < blocks_a)
+        combine_block<LPR, NV>(a, blk);
     else
-        combine_row<LPR, NV>(b, s - a.n_splits);
+        combine_block<LPR, NV>(b, blk - blocks_a);
 }
 
 // ---- generic path: any d <= 64*KMAX, one wave per item, scalar columns ----
@@ -571,7 +613,8 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass, const SpmmArgs* b = n
             }
         }
         if ((pass & PASS_COMBINE) && a.n_splits + b->n_splits > 0) {
-            k_combine_pair<LPR, NV><<<dim3(static_cast<unsigned>(a.n_splits + b->n_splits)), kBlock, 0, s>>>(a, *b);
+            const int64_t ca = combine_blocks<LPR, NV>(a), cb = combine_blocks<LPR, NV>(*b);
+            k_combine_pair<LPR, NV><<<dim3(static_cast<unsigned>(ca + cb)), kBlock, 0, s>>>(a, *b, ca);
             if (int rc = check_launch("k_combine_pair")) return rc;
         }
         return LGCN_OK;
@@ -856,9 +899,13 @@ int lgcn_spmm_pair(const lgcn_pass_t* a, const lgcn_pass_t* b, int64_t N, int32_
                                 p.e_hi, p.e_split, p.acc_lo, p.acc_hi, p.acc_split, p.partial, p.mode, PASS_BOTH,
                                 nullptr))
             return rc;
+        if (p.n_split_big > p.n_splits)
+            return fail(LGCN_E_ARG, "lgcn_spmm_pair: n_split_big %lld > n_splits %lld", (long long)p.n_split_big,
+                        (long long)p.n_splits);
         args[i] = SpmmArgs{p.items, p.n_items, p.splits, p.n_splits, p.col, p.val, p.x_lo, p.x_hi, p.x_split,
                            p.e_lo, p.e_hi, p.e_split, p.y, p.acc_lo, p.acc_hi, p.acc_split, p.partial, d, p.mode,
                            p.div, p.mul, nullptr, nullptr};
+        args[i].n_big = p.n_split_big < 0 ? -1 : p.n_split_big;
     }
     if (N == 0) return LGCN_OK;
     return dispatch(args[0], N, as_stream(stream), what, nullptr, &args[1]);

@@ -141,7 +141,11 @@ class Pass(ctypes.Structure):
                 ("e_lo", ctypes.c_void_p), ("e_hi", ctypes.c_void_p), ("e_split", ctypes.c_int64),
                 ("y", ctypes.c_void_p), ("acc_lo", ctypes.c_void_p), ("acc_hi", ctypes.c_void_p),
                 ("acc_split", ctypes.c_int64), ("partial", ctypes.c_void_p), ("mode", ctypes.c_int32),
-                ("div", ctypes.c_float), ("mul", ctypes.c_float)]
+                ("div", ctypes.c_float), ("mul", ctypes.c_float), ("n_split_big", ctypes.c_int64)]
+
+    def __init__(self, *args, n_split_big: int = -1, **kw):
+        super().__init__(*args, **kw)
+        self.n_split_big = n_split_big
 
 
 class LgcnError(RuntimeError):

@@ -112,6 +112,26 @@ class CsrDirection:
         return torch.stack([it[:, 0], lens_dst[:, 0].long(), lens_dst[:, 1].long()], dim=1)
 
 
+SMALL_SPLIT_CHUNKS = 16  # kVSums (csrc/lgcn_spmm.hip): a split row of <= this many chunks combines in a lane group
+
+
+def pack_split_rows(direction: CsrDirection) -> int:
+    """Order the direction's split rows big-first (more than SMALL_SPLIT_CHUNKS chunks) and record
+    how many are big (direction.n_split_big, lgcn_pass_t.n_split_big): the pair combine then gives
+    each big row a workgroup and packs the small ones one per lane group. The combine reads a row's
+    partials through its split record, so the order changes nothing else (one host sync)."""
+    n = direction.n_splits
+    if n == 0:
+        direction.n_split_big = 0
+        return 0
+    sp = direction.splits[:n]
+    big = sp[:, 2] > SMALL_SPLIT_CHUNKS
+    order = torch.argsort((~big).to(torch.int8), stable=True)
+    direction.splits[:n] = sp[order].clone()
+    direction.n_split_big = int(big.sum().item())
+    return direction.n_split_big
+
+
 def _schedule(rowptr: torch.Tensor, N: int, E: int, chunk: int, side_split: int, row_mask, stream: int):
     lib = _ffi.load()
     dev = rowptr.device

@@ -569,6 +569,11 @@ class ReducePlan:
         self.partial, _, _ = _build_direction(dst[sel].contiguous(), src[sel].contiguous(), N, self.chunk, U,
                                               self.dis, stream, items)
         self.partial.block_split = False
+        # the pair combine (fused order) packs the thousands of 2-16-chunk split rows by lane group
+        from .plan import pack_split_rows
+
+        pack_split_rows(self.users)
+        pack_split_rows(self.partial)
         # the last layer's item rows are reduce-scattered: this group's share of the items
         # (I padded to a multiple of R; padding rows are zero partials that no pass writes)
         R = shards.R
@@ -622,7 +627,8 @@ class ReducePlan:
             return _ffi.Pass(direction.items.data_ptr(), direction.n_items, direction.splits.data_ptr(),
                              direction.n_splits, direction.col.data_ptr(), direction.val.data_ptr(),
                              _ffi.ptr(x[0]), _ffi.ptr(x[1]), x[2], _ffi.ptr(ee[0]), _ffi.ptr(ee[1]), ee[2],
-                             _ffi.ptr(y_), _ffi.ptr(a_lo), _ffi.ptr(a_hi), a_split, _ffi.ptr(part), m, dv, ml)
+                             _ffi.ptr(y_), _ffi.ptr(a_lo), _ffi.ptr(a_hi), a_split, _ffi.ptr(part), m, dv, ml,
+                             n_split_big=getattr(direction, "n_split_big", -1))
 
         pa = pass_of(self.partial, (x_users, part_items, U), (None, None, N), None, part_items, part_items, U,
                      _ffi.EPI_STORE, 1.0, 1.0)

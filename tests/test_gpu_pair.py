@@ -30,24 +30,29 @@ def _direction(dev, ei, N, chunk, side_split):
     return d
 
 
-def _pass(direction, x, y, acc, part, mode, e=None, div=1.0, mul=1.0):
+def _pass(direction, x, y, acc, part, mode, e=None, div=1.0, mul=1.0, packed=False):
     from lgcn_amd import _ffi
 
     N = x.shape[0]
     return _ffi.Pass(direction.items.data_ptr(), direction.n_items, direction.splits.data_ptr(), direction.n_splits,
                      direction.col.data_ptr(), direction.val.data_ptr(), x.data_ptr(), None, N,
-                     _ffi.ptr(e), None, N, _ffi.ptr(y), acc.data_ptr(), None, N, _ffi.ptr(part), mode, div, mul)
+                     _ffi.ptr(e), None, N, _ffi.ptr(y), acc.data_ptr(), None, N, _ffi.ptr(part), mode, div, mul,
+                     n_split_big=direction.n_split_big if packed else -1)
 
 
 @pytest.mark.parametrize("d", [4, 8, 16, 32, 64, 128, 256, 512])
-@pytest.mark.parametrize("chunk,xcd", [(8, "0"), (4096, "0"), (8, "1"), (4096, "1")])
-def test_spmm_pair_bitwise_single_passes(gpu, monkeypatch, d, chunk, xcd):
+@pytest.mark.parametrize("chunk,xcd,packed", [(8, "0", False), (4096, "0", False), (8, "1", False),
+                                              (4096, "1", False), (8, "1", True), (2, "1", True)])
+def test_spmm_pair_bitwise_single_passes(gpu, monkeypatch, d, chunk, xcd, packed):
     """xcd = LGCN_PAIR_XCD: the XCD-split block mapping (each pass on half the XCDs while both have
-    blocks left) gives the same rows."""
+    blocks left) gives the same rows; packed: split rows ordered big-first (pack_split_rows) and the
+    <= 16-chunk ones combined one per lane group — the same rows too (chunk 2: hub rows of
+    hundreds of chunks beside small ones)."""
     import graphs
 
     monkeypatch.setenv("LGCN_PAIR_XCD", xcd)
     from lgcn_amd import _ffi
+    from lgcn_amd.plan import pack_split_rows
     from lgcn_amd.propagate import spmm
 
     U, I, ei_a = graphs.hub(U=1500, I=40, seed=1)
@@ -55,6 +60,11 @@ def test_spmm_pair_bitwise_single_passes(gpu, monkeypatch, d, chunk, xcd):
     _, _, ei_b = graphs.subsampled(U=U, I=I, pairs=9000, seed=3)
     da = _direction(gpu, ei_a, N, chunk, U)
     db = _direction(gpu, ei_b, N, chunk, 0)
+    if packed:
+        nb_a, nb_b = pack_split_rows(da), pack_split_rows(db)
+        assert da.n_splits > nb_a  # some small rows to pack
+        if chunk == 2:
+            assert nb_a > 0  # and big ones beside them
     g = torch.Generator(device=gpu).manual_seed(d)
     xa = torch.randn(N, d, device=gpu, generator=g)
     xb = torch.randn(N, d, device=gpu, generator=g)
@@ -68,15 +78,15 @@ def test_spmm_pair_bitwise_single_passes(gpu, monkeypatch, d, chunk, xcd):
         pa_ = torch.empty((max(1, da.n_partials), d), device=gpu)
         pb_ = torch.empty((max(1, db.n_partials), d), device=gpu)
         if paired:
-            pa = _pass(da, xa, None, acc_a, pa_, _ffi.EPI_STORE)
-            pb = _pass(db, xb, y_b, acc_b, pb_, _ffi.EPI_INIT, e=e)
+            pa = _pass(da, xa, None, acc_a, pa_, _ffi.EPI_STORE, packed=packed)
+            pb = _pass(db, xb, y_b, acc_b, pb_, _ffi.EPI_INIT, e=e, packed=packed)
             _ffi.check(lib.lgcn_spmm_pair(ctypes.byref(pa), ctypes.byref(pb), N, d, 1, _ffi.stream_of(gpu)), "pair")
             _ffi.check(lib.lgcn_spmm_pair(ctypes.byref(pa), ctypes.byref(pb), N, d, 2, _ffi.stream_of(gpu)), "pair")
         else:
             spmm(da, N, d, (xa, None, N), None, (acc_a, None, N), None, _ffi.EPI_STORE, 1.0, 1.0, pa_)
             spmm(db, N, d, (xb, None, N), (e, None, N), (acc_b, None, N), y_b, _ffi.EPI_INIT, 1.0, 1.0, pb_)
         outs.append((acc_a.cpu(), acc_b.cpu(), y_b.cpu()))
-    if chunk == 8:
+    if chunk <= 8:
         assert da.n_splits > 0 and db.n_splits > 0
     for one, two in zip(*outs):
         assert torch.equal(one, two)
@@ -92,6 +102,8 @@ def test_spmm_pair_argument_errors(gpu):
     p.n_items, p.mode = 1, 9
     assert lib.lgcn_spmm_pair(ctypes.byref(p), ctypes.byref(p), 4, 8, 1, None) == _ffi.E_ARG
     assert b"bad mode" in lib.lgcn_last_error()
+    p.mode, p.n_splits, p.n_split_big = 0, 2, 3
+    assert lib.lgcn_spmm_pair(ctypes.byref(p), ctypes.byref(p), 4, 8, 1, None) == _ffi.E_ARG
 
 
 @pytest.mark.parametrize("K", [1, 2, 3, 4])

@@ -2,7 +2,7 @@
 ReducePlan: users sharded, item partials all-reduced) on one GPU, per R x F grid, without the
 all_reduce (a stand-in reducer that moves nothing): the time a rank spends in its kernels per K=3
 step, next to the bytes a ring all_reduce of its item partials moves per rank.
-python tools/reduce_rank_probe.py [--grids 2x1,4x1,8x1,2x2,4x2,2x4] [--orders overlapped,fused]"""
+python tools/reduce_rank_probe.py [--grids 2x1,4x1,8x1,2x2,4x2,2x4] [--orders overlapped,fused,fused-seq]"""
 import argparse
 import os
 import sys
@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--grids", default="2x1,4x1,8x1,2x2,4x2,2x4")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--chunk", type=int, default=256)
-    ap.add_argument("--orders", default="overlapped,fused,fusedx")
+    ap.add_argument("--orders", default="overlapped,fused,fused-seq")
     args = ap.parse_args()
     dev = torch.device("cuda")
     g = synth.ml25m_shaped(seed=0)
@@ -64,8 +64,8 @@ def main():
             red = NoReduce(R)
             for order in times:
                 fused = order.startswith("fused")
-                # fusedx: the pair launch's XCD-split block mapping (LGCN_PAIR_XCD=1)
-                os.environ["LGCN_PAIR_XCD"] = "1" if order == "fusedx" else "0"
+                # fused-seq: the pair launch without its XCD-split block mapping (LGCN_PAIR_XCD=0)
+                os.environ["LGCN_PAIR_XCD"] = "0" if order == "fused-seq" else "1"
                 with torch.no_grad():
                     for _ in range(3):
                         propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)
