@@ -81,3 +81,23 @@ def test_recall_upper_bound():
     embs = tuple(torch.from_numpy(rng.standard_normal((500, 8)).astype(np.float32)) for _ in range(3))
     np.random.seed(0)
     assert TT.compute_recall_at_k(embs, k=20) <= 20 / 500 + 1e-12
+
+
+def test_train_routes_cpu_models_to_the_reference_loop():
+    """The package's train() runs the fused batch step only for a HIP LightGCN with the reference's
+    torch Adam (lgcn_amd.harness.eligibility); a CPU model takes the reference loop — bitwise the
+    reference's results (test_train_epoch_matches_reference) — and the harness says why."""
+    _trained_model()
+    assert TT.LAST_TRAIN_PATH == "reference: model not on a ROCm device"
+
+
+def test_fused_harness_eligibility_reasons():
+    from lgcn_amd import harness
+
+    model = OracleLightGCN(10, 8, num_layers=2, dim_h=16)
+    assert "ROCm" in harness.eligibility(model, torch.optim.Adam(model.parameters(), lr=1e-3))
+
+    class Bare(torch.nn.Module):
+        pass
+
+    assert "not a LightGCN" in harness.eligibility(Bare(), None)
