@@ -302,10 +302,6 @@ typedef struct {
 } lgcn_pass_t;
 int lgcn_spmm_pair(const lgcn_pass_t* a, const lgcn_pass_t* b, int64_t N, int32_t d, int32_t what,
                    lgcn_stream_t stream);
-/* One pass described by a lgcn_pass_t: what = 1 its item pass, 2 its combine, 3 both — lgcn_spmm_items /
- * lgcn_spmm_combine / lgcn_spmm, plus the packed combine when n_split_big >= 0 (the one-GPU
- * source-sliced schedule's hub rows, lgcn_amd/sliced.py). Same reference code as lgcn_spmm. */
-int lgcn_spmm_pass(const lgcn_pass_t* a, int64_t N, int32_t d, int32_t what, lgcn_stream_t stream);
 
 /* The layer-stack mean of rows whose layer outputs were kept instead of accumulated (ABI 5):
  * out[r] = ((((e[r] + y_0[r]) + y_1[r]) + ... + y_{K-1}[r]) / div) * mul for r in [0, rows) — the

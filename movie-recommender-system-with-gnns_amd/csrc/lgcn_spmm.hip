@@ -516,12 +516,6 @@ __device__ __forceinline__ void combine_block(const SpmmArgs& a, int64_t blk) {
     if (s < a.n_splits) combine_small_row<LPR, NV>(a, s, threadIdx.x % LPR);
 }
 
-// One pass's split rows, big rows a workgroup each, then the small ones by lane group (n_big >= 0).
-template <int LPR, int NV>
-__global__ __launch_bounds__(kBlock) void k_combine_packed(SpmmArgs a) {
-    combine_block<LPR, NV>(a, blockIdx.x);
-}
-
 // The split rows of two passes in one launch: a's workgroups first, then b's.
 template <int LPR, int NV>
 __global__ __launch_bounds__(kBlock) void k_combine_pair(SpmmArgs a, SpmmArgs b, int64_t blocks_a) {
@@ -642,13 +636,8 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass, const SpmmArgs* b = n
         if (int rc = check_launch("k_spmm_vec")) return rc;
     }
     if ((pass & PASS_COMBINE) && a.n_splits > 0) {
-        if (a.n_big >= 0) {  // lgcn_spmm_pass with a packed split list
-            k_combine_packed<LPR, NV><<<dim3(static_cast<unsigned>(combine_blocks<LPR, NV>(a))), kBlock, 0, s>>>(a);
-            if (int rc = check_launch("k_combine_packed")) return rc;
-        } else {
-            k_combine_vec<LPR, NV><<<dim3(static_cast<unsigned>(a.n_splits)), kBlock, 0, s>>>(a);
-            if (int rc = check_launch("k_combine_vec")) return rc;
-        }
+        k_combine_vec<LPR, NV><<<dim3(static_cast<unsigned>(a.n_splits)), kBlock, 0, s>>>(a);
+        if (int rc = check_launch("k_combine_vec")) return rc;
     }
     return LGCN_OK;
 }
@@ -920,25 +909,6 @@ int lgcn_spmm_pair(const lgcn_pass_t* a, const lgcn_pass_t* b, int64_t N, int32_
     }
     if (N == 0) return LGCN_OK;
     return dispatch(args[0], N, as_stream(stream), what, nullptr, &args[1]);
-}
-
-int lgcn_spmm_pass(const lgcn_pass_t* a, int64_t N, int32_t d, int32_t what, lgcn_stream_t stream) {
-    if (!a || what < 1 || what > 3) return fail(LGCN_E_ARG, "lgcn_spmm_pass: bad args");
-    const lgcn_pass_t& p = *a;
-    if (int rc = check_pass(p.items, p.n_items, p.splits, p.n_splits, N, d, p.x_lo, p.x_hi, p.x_split, p.e_lo, p.e_hi,
-                            p.e_split, p.acc_lo, p.acc_hi, p.acc_split, p.partial, p.mode, PASS_BOTH, nullptr))
-        return rc;
-    if (p.n_split_big > p.n_splits)
-        return fail(LGCN_E_ARG, "lgcn_spmm_pass: n_split_big %lld > n_splits %lld", (long long)p.n_split_big,
-                    (long long)p.n_splits);
-    if (N == 0 || (p.n_items == 0 && p.n_splits == 0)) return LGCN_OK;
-    SpmmArgs args{p.items, p.n_items, p.splits, p.n_splits, p.col, p.val, p.x_lo, p.x_hi, p.x_split, p.e_lo, p.e_hi,
-                  p.e_split, p.y, p.acc_lo, p.acc_hi, p.acc_split, p.partial, d, p.mode, p.div, p.mul, nullptr,
-                  nullptr};
-    args.n_big = p.n_split_big < 0 ? -1 : p.n_split_big;
-    if (args.n_big >= 0 && !vec_aligned(args))
-        return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm_pass: a packed split list needs d in {4,8,...,1024}, aligned rows");
-    return dispatch(args, N, as_stream(stream), what, nullptr, nullptr);
 }
 
 int lgcn_stack_mean_rows(const float* e, const float* const* ys, int32_t K, int64_t rows, int32_t d, float* out,

@@ -68,7 +68,6 @@ _SIGS = {
                               _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp],
                              ctypes.c_int),
     "lgcn_spmm_pair": ([_vp, _vp, _i64, _i32, _i32, _vp], ctypes.c_int),
-    "lgcn_spmm_pass": ([_vp, _i64, _i32, _i32, _vp], ctypes.c_int),
     "lgcn_stack_mean_rows": ([_vp, _vp, _i32, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_scale": ([_vp, _vp, _i64, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_copy_scale": ([_vp, _vp, _i64, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),

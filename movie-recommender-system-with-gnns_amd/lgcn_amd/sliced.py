@@ -13,9 +13,7 @@ once per (edge set, width).
 """
 from __future__ import annotations
 
-import ctypes
 import dataclasses
-import os
 
 import torch
 
@@ -37,7 +35,6 @@ class SlicedDirection:
     bounds: list            # source-id slice boundaries
     items: torch.Tensor = None       # all items, slice-major (launches are views of it)
     host_offsets: object = None      # ctypes int64[S+1]: slice s = items[off[s]:off[s+1]]
-    n_split_big: int = -1            # >= 0: splits packed big-first (plan.pack_split_rows)
 
     @property
     def n_launches(self) -> int:
@@ -99,13 +96,8 @@ def build_sliced(f: CsrDirection, N: int, bounds: list[int], chunk: int = 256,
     if unsorted:
         return None
     launches = [(items[off[s]:off[s + 1]], off[s + 1] - off[s]) for s in range(S)]
-    sd = SlicedDirection(f, launches, splits, n_splits, n_partials, list(bounds), items,
-                         (ctypes.c_int64 * (S + 1))(*off))
-    if os.environ.get("LGCN_PACKED_COMBINE", "1") != "0":
-        from .plan import pack_split_rows
-
-        pack_split_rows(sd)  # the hub combine: <= 16-chunk hubs one per lane group
-    return sd
+    return SlicedDirection(f, launches, splits, n_splits, n_partials, list(bounds), items,
+                           (ctypes.c_int64 * (S + 1))(*off))
 
 
 def _tail(sd: SlicedDirection, N, d, x, e, acc, y, mode, div, mul, partial, stream):
@@ -141,15 +133,6 @@ def spmm_sliced_combine(sd: SlicedDirection, N: int, d: int, x, e, acc, y, mode:
                         partial: torch.Tensor | None, stream: int) -> None:
     if sd.n_splits:
         lib = _ffi.load()
-        if sd.n_split_big >= 0 and d % 4 == 0:  # packed: the lane-group combine of the small hubs
-            xl, xh, xs = x
-            el, eh, es = e if e is not None else (None, None, N)
-            al, ah, as_ = acc
-            p = _ffi.Pass(None, 0, sd.splits.data_ptr(), sd.n_splits, _ffi.ptr(sd.base.col), _ffi.ptr(sd.base.val),
-                          _ffi.ptr(xl), _ffi.ptr(xh), xs, _ffi.ptr(el), _ffi.ptr(eh), es, _ffi.ptr(y), _ffi.ptr(al),
-                          _ffi.ptr(ah), as_, _ffi.ptr(partial), mode, div, mul, n_split_big=sd.n_split_big)
-            _ffi.check(lib.lgcn_spmm_pass(ctypes.byref(p), N, d, 2, stream), "lgcn_spmm_pass(combine)")
-            return
         tail = _tail(sd, N, d, x, e, acc, y, mode, div, mul, partial, stream)
         _ffi.check(lib.lgcn_spmm_combine(None, 0, sd.splits.data_ptr(), sd.n_splits, *tail), "lgcn_spmm_combine")
 

@@ -3,10 +3,11 @@ reference-style loop (autograd + torch Adam + clip_grad_norm_, LGCN_HARNESS_FUSE
 batch step it routes to by default (lgcn_amd.harness: HIP forward / BPR / backward, exact row-lazy
 Adam, one hipGraph per batch). Same model init, same seed, so the same negatives: the epoch loss
 within 1e-5, and after every epoch the tables and Adam moments within 1e-5 per row on the elements
-whose Adam steps are well conditioned (_settled: every step's gradient clear of the per-row
-gradient bar by 10x, and the first moment not a near-cancellation of earlier gradients, which
-would amplify the gradients' 1e-6-level summation-order differences; those elements are counted
-and printed), the second moments within 1e-5 per row everywhere, the
+whose Adam steps are well conditioned (_settled: every step's gradient within 1e-2 of its row's
+largest, and the first moment not a near-cancellation of earlier gradients — Adam steps every
+element by about lr, so an element's relative gradient error, the paths' 1e-6-of-the-row
+summation-order differences divided by the element's share of the row, is what reaches its
+weight; those elements are counted and printed), the second moments within 1e-5 per row everywhere, the
 rows that move identical, the step counts equal.
 Epoch 2 starts from the torch optimizer state epoch 1 wrote back (the paths can alternate)."""
 import numpy as np
@@ -78,9 +79,11 @@ def _settled(grads, frac=0.05):
             m[t] = 0.9 * m[t] + 0.1 * c * g
             a[t] = 0.9 * a[t] + 0.1 * c * np.abs(g)
             ok[t] &= np.abs(m[t]) >= frac * a[t]
-            # and each step's gradient clear of the per-row 1e-5 gradient bar by 10x (or exactly 0):
-            # a noise-level gradient's relative error is its own, not the row's
-            ok[t] &= (g == 0) | (np.abs(g) > 1e-4 * np.abs(g).max(axis=1, keepdims=True))
+            # and each step's gradient at least 1e-2 of its row's largest (or exactly 0): the two
+            # paths' gradients agree to ~1e-6 of the ROW's scale, so an element 1e-2 below it has a
+            # relative error up to 1e-4 — and Adam moves every element by about lr whatever its size,
+            # so smaller elements' steps carry their larger relative errors into the weights
+            ok[t] &= (g == 0) | (np.abs(g) > 1e-2 * np.abs(g).max(axis=1, keepdims=True))
     return ok
 
 
