@@ -382,29 +382,32 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
 // [0, blocks_a) run pass a, the rest pass b. Each pass keeps its own longest-first order, and b's
 // longest items start while a's last workgroups drain, so the pair pays one launch gap and one
 // drain instead of two. Per row the arithmetic is the single pass's (bitwise).
-// split_xcd (the default): workgroups are dealt to the 8 XCDs round-robin (workgroup i on XCD i % 8), so while
-// both passes have blocks left, pass a takes the slots of XCDs 0-3 and pass b those of XCDs 4-7 —
-// each XCD's L2 then holds one pass's gather table instead of both — and the longer pass's
-// remaining blocks follow on every XCD.
+// xcd_a (1..7, default 4): workgroups are dealt to the 8 XCDs round-robin (workgroup i on XCD
+// i % 8), so while both passes have blocks left, pass a takes the slots of XCDs [0, xcd_a) and
+// pass b those of XCDs [xcd_a, 8) — each XCD's L2 then caches one pass's gather table instead of
+// both — and the longer pass's remaining blocks follow on every XCD. xcd_a = 0: a's blocks, then
+// b's, on every XCD.
 template <int LPR, int NV, int UNROLL, int TAIL, int CM>
 __global__ __launch_bounds__(kBlock) void k_spmm_pair(SpmmArgs a, SpmmArgs b, int64_t blocks_a, int64_t blocks_b,
-                                                      int split_xcd) {
+                                                      int xcd_a) {
     const int64_t blk = blockIdx.x;
-    if (split_xcd) {
-        const int64_t m = (blocks_a < blocks_b ? blocks_a : blocks_b) & ~int64_t(3);  // 4 per round each
-        if (blk < 2 * m) {
+    if (xcd_a > 0) {
+        const int64_t sa = xcd_a, sb = 8 - xcd_a;
+        const int64_t ra = blocks_a / sa, rb = blocks_b / sb;
+        const int64_t rounds = ra < rb ? ra : rb;  // rounds of 8 with both passes present
+        if (blk < 8 * rounds) {
             const int64_t k = blk >> 3, x = blk & 7;
-            if (x < 4)
-                item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(a, k * 4 + x);
+            if (x < sa)
+                item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(a, k * sa + x);
             else
-                item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(b, k * 4 + x - 4);
+                item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(b, k * sb + x - sa);
             return;
         }
-        const int64_t r = blk - 2 * m;  // the rest of both, a's first
-        if (r < blocks_a - m)
-            item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(a, m + r);
+        const int64_t r = blk - 8 * rounds, left_a = blocks_a - rounds * sa;  // the rest, a's first
+        if (r < left_a)
+            item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(a, rounds * sa + r);
         else
-            item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(b, m + r - (blocks_a - m));
+            item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(b, rounds * sb + r - left_a);
         return;
     }
     if (blk < blocks_a)
@@ -413,11 +416,13 @@ __global__ __launch_bounds__(kBlock) void k_spmm_pair(SpmmArgs a, SpmmArgs b, in
         item_pass<LPR, NV, UNROLL, false, TAIL, false, CM>(b, blk - blocks_a);
 }
 
-// lgcn_spmm_pair's XCD-split block mapping: on by default (reduce-mode 4 x 2 rank step, K=3, C2:
-// 0.193 -> 0.176 ms; 8 x 1 0.182 vs 0.184, profiles/r04a_pair/); LGCN_PAIR_XCD=0 turns it off.
-int pair_split_xcd() {
+// lgcn_spmm_pair's XCDs for pass a: 4 by default (reduce-mode 4 x 2 rank step, K=3, C2: 0.193 ->
+// 0.176 ms against a's blocks then b's; 8 x 1 0.182 vs 0.184, profiles/r04a_pair/);
+// LGCN_PAIR_XCD = 0 (sequential) or 1..7 overrides (A/B).
+int pair_xcd_a() {
     const char* v = std::getenv("LGCN_PAIR_XCD");
-    return v ? std::atoi(v) : 1;
+    const int x = v ? std::atoi(v) : 4;
+    return x < 0 || x > 7 ? 4 : x;
 }
 
 // Split rows: one workgroup per split row. Running sum v (of kVSums, owned by lane group v % GPB)
@@ -608,7 +613,7 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass, const SpmmArgs* b = n
             const int64_t ba = (a.n_items + GPB - 1) / GPB, bb = (b->n_items + GPB - 1) / GPB;
             if (ba + bb > 0) {
                 k_spmm_pair<LPR, NV, UNROLL, TAIL, CM><<<dim3(static_cast<unsigned>(ba + bb)), kBlock, 0, s>>>(
-                    a, *b, ba, bb, pair_split_xcd());
+                    a, *b, ba, bb, pair_xcd_a());
                 if (int rc = check_launch("k_spmm_pair")) return rc;
             }
         }

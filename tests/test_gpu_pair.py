@@ -41,11 +41,12 @@ def _pass(direction, x, y, acc, part, mode, e=None, div=1.0, mul=1.0, packed=Fal
 
 
 @pytest.mark.parametrize("d", [4, 8, 16, 32, 64, 128, 256, 512])
-@pytest.mark.parametrize("chunk,xcd,packed", [(8, "0", False), (4096, "0", False), (8, "1", False),
-                                              (4096, "1", False), (8, "1", True), (2, "1", True)])
+@pytest.mark.parametrize("chunk,xcd,packed", [(8, "0", False), (4096, "0", False), (8, "4", False),
+                                              (4096, "4", False), (8, "4", True), (2, "4", True), (8, "3", True),
+                                              (8, "7", False)])
 def test_spmm_pair_bitwise_single_passes(gpu, monkeypatch, d, chunk, xcd, packed):
-    """xcd = LGCN_PAIR_XCD: the XCD-split block mapping (each pass on half the XCDs while both have
-    blocks left) gives the same rows; packed: split rows ordered big-first (pack_split_rows) and the
+    """xcd = LGCN_PAIR_XCD: the XCD-split block mapping (pass a on xcd of the 8 XCDs, b on the rest,
+    while both have blocks left; 0 = a's blocks then b's) gives the same rows; packed: split rows ordered big-first (pack_split_rows) and the
     <= 16-chunk ones combined one per lane group — the same rows too (chunk 2: hub rows of
     hundreds of chunks beside small ones)."""
     import graphs

@@ -64,8 +64,10 @@ def main():
             red = NoReduce(R)
             for order in times:
                 fused = order.startswith("fused")
-                # fused-seq: the pair launch without its XCD-split block mapping (LGCN_PAIR_XCD=0)
-                os.environ["LGCN_PAIR_XCD"] = "0" if order == "fused-seq" else "1"
+                # fused-seq: the pair launch without its XCD-split block mapping (LGCN_PAIR_XCD=0);
+                # fusedN: pass a (the item partials) on N of the 8 XCDs
+                os.environ["LGCN_PAIR_XCD"] = ("0" if order == "fused-seq" else
+                                               order[5:] if order[5:].isdigit() else "4")
                 with torch.no_grad():
                     for _ in range(3):
                         propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)
