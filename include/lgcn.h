@@ -303,6 +303,11 @@ typedef struct {
 int lgcn_spmm_pair(const lgcn_pass_t* a, const lgcn_pass_t* b, int64_t N, int32_t d, int32_t what,
                    lgcn_stream_t stream);
 
+/* One plain pass described by an lgcn_pass_t (what = 1 item pass, 2 combine, 3 both): lgcn_spmm
+ * with the packed combine of n_split_big — bitwise lgcn_spmm's rows. The reduce-mode forward's
+ * overlapped order runs its passes one at a time through this (ABI 5). Any d lgcn_spmm takes. */
+int lgcn_spmm_pass(const lgcn_pass_t* p, int64_t N, int32_t d, int32_t what, lgcn_stream_t stream);
+
 /* The layer-stack mean of rows whose layer outputs were kept instead of accumulated (ABI 5):
  * out[r] = ((((e[r] + y_0[r]) + y_1[r]) + ... + y_{K-1}[r]) / div) * mul for r in [0, rows) — the
  * additions and roundings of the INIT, ADD..., FINAL_ACC epilogue sequence (K == 1: FINAL_E), so

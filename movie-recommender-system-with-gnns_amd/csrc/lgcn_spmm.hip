@@ -426,14 +426,18 @@ int pair_xcd_a() {
 }
 
 // Split rows: one workgroup per split row. Running sum v (of kVSums, owned by lane group v % GPB)
-// adds partials v, v + kVSums, ... with UNROLL loads in flight; the kVSums sums are then added in
-// v order through LDS. The association is fixed by the code and the same at every width, so
-// results are deterministic run to run and a column share is bitwise the full row's share.
+// adds partials v, v + kVSums, ... in that order; the kVSums sums are then added in v order through
+// LDS. The association is fixed by the code and the same at every width, so results are
+// deterministic run to run and a column share is bitwise the full row's share.
+// The partials of a sum are loaded kCombineBatch at a time, all issued (predicated past pcnt) before
+// the first add, so a sum of n partials waits ceil(n / kCombineBatch) memory round trips instead of
+// one per partial — the combine launch is a chain of dependent loads, not a bandwidth problem.
+constexpr int kCombineBatch = 8;
+
 template <int LPR, int NV>
 __device__ __forceinline__ void combine_row(const SpmmArgs& a, int64_t s) {
     constexpr int GPB = kBlock / LPR;
     constexpr int VPG = (kVSums + GPB - 1) / GPB;
-    constexpr int UNROLL = 4;
     __shared__ float4 lds[kVSums][LPR * NV];
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
@@ -448,21 +452,19 @@ __device__ __forceinline__ void combine_row(const SpmmArgs& a, int64_t s) {
         float4 acc[NV];
 #pragma unroll
         for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        int c = v;
-        for (; c + (UNROLL - 1) * kVSums < sp.pcnt; c += UNROLL * kVSums) {
-            float4 t[UNROLL][NV];
+        for (int c = v; c < sp.pcnt; c += kCombineBatch * kVSums) {
+            float4 t[kCombineBatch][NV];
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
+            for (int u = 0; u < kCombineBatch; ++u)
+                if (c + u * kVSums < sp.pcnt)
 #pragma unroll
-                for (int k = 0; k < NV; ++k) t[u][k] = p[int64_t(c + u * kVSums) * d4 + l + k * LPR];
+                    for (int k = 0; k < NV; ++k) t[u][k] = p[int64_t(c + u * kVSums) * d4 + l + k * LPR];
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
+            for (int u = 0; u < kCombineBatch; ++u)
+                if (c + u * kVSums < sp.pcnt)
 #pragma unroll
-                for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], t[u][k]);
+                    for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], t[u][k]);
         }
-        for (; c < sp.pcnt; c += kVSums)
-#pragma unroll
-            for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], p[int64_t(c) * d4 + l + k * LPR]);
 #pragma unroll
         for (int k = 0; k < NV; ++k) lds[v][l + k * LPR] = acc[k];
     }
@@ -485,19 +487,29 @@ __global__ __launch_bounds__(kBlock) void k_combine_vec(SpmmArgs a) {
 
 // A split row of at most kVSums chunks, combined by one lane group: running sum v holds partial v
 // alone (0 + p_v), and the sums are added in v order — combine_row's association for such a row,
-// so bitwise its result — without a workgroup, LDS or a barrier per row.
+// so bitwise its result — without a workgroup, LDS or a barrier per row. All of the row's partials
+// are loaded (predicated past pcnt) before the first add: one memory round trip, not pcnt.
 template <int LPR, int NV>
 __device__ __forceinline__ void combine_small_row(const SpmmArgs& a, int64_t s, int l) {
+    constexpr int B = NV == 1 ? kVSums : kCombineBatch;  // partials in flight (registers: B * NV float4)
     const lgcn_split_t sp = a.splits[s];
     const int64_t d4 = int64_t(LPR) * NV;
     const float4* p = reinterpret_cast<const float4*>(a.partial) + int64_t(sp.pbeg) * d4 + l;
     const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 acc[NV];
+    for (int c0 = 0; c0 < sp.pcnt; c0 += B) {
+        float4 t[B][NV];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] = f4_add(zero, p[k * LPR]);
-    for (int c = 1; c < sp.pcnt; ++c)
+        for (int u = 0; u < B; ++u)
+            if (c0 + u < sp.pcnt)
 #pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] = f4_add(acc[k], f4_add(zero, p[int64_t(c) * d4 + k * LPR]));
+                for (int k = 0; k < NV; ++k) t[u][k] = p[int64_t(c0 + u) * d4 + k * LPR];
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+            if (c0 + u < sp.pcnt)
+#pragma unroll
+                for (int k = 0; k < NV; ++k) acc[k] = c0 + u == 0 ? f4_add(zero, t[u][k]) : f4_add(acc[k], f4_add(zero, t[u][k]));
+    }
     finish_row_vec<LPR, NV>(a, sp.row, l, acc);
 }
 
@@ -519,6 +531,12 @@ __device__ __forceinline__ void combine_block(const SpmmArgs& a, int64_t blk) {
     }
     const int64_t s = big + (blk - big) * GPB + threadIdx.x / LPR;
     if (s < a.n_splits) combine_small_row<LPR, NV>(a, s, threadIdx.x % LPR);
+}
+
+// The split rows of one pass, packed (a.n_big >= 0: lgcn_spmm_pass).
+template <int LPR, int NV>
+__global__ __launch_bounds__(kBlock) void k_combine_packed(SpmmArgs a) {
+    combine_block<LPR, NV>(a, blockIdx.x);
 }
 
 // The split rows of two passes in one launch: a's workgroups first, then b's.
@@ -641,6 +659,10 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass, const SpmmArgs* b = n
         if (int rc = check_launch("k_spmm_vec")) return rc;
     }
     if ((pass & PASS_COMBINE) && a.n_splits > 0) {
+        if (a.n_big >= 0) {  // lgcn_spmm_pass with n_split_big: the small rows one per lane group
+            k_combine_packed<LPR, NV><<<dim3(static_cast<unsigned>(combine_blocks<LPR, NV>(a))), kBlock, 0, s>>>(a);
+            return check_launch("k_combine_packed");
+        }
         k_combine_vec<LPR, NV><<<dim3(static_cast<unsigned>(a.n_splits)), kBlock, 0, s>>>(a);
         if (int rc = check_launch("k_combine_vec")) return rc;
     }
@@ -893,27 +915,37 @@ int lgcn_spmm_blocksplit(LGCN_SPMM_PARAMS, const lgcn_item_t* chunks) {
     return spmm_impl(LGCN_SPMM_ARGS, PASS_BSPLIT, nullptr, chunks);
 }
 
+// lgcn_pass_t -> SpmmArgs, validated as a plain pass of width d over N rows.
+static int pass_args(const lgcn_pass_t& p, int64_t N, int32_t d, const char* who, SpmmArgs& out) {
+    if (int rc = check_pass(p.items, p.n_items, p.splits, p.n_splits, N, d, p.x_lo, p.x_hi, p.x_split, p.e_lo,
+                            p.e_hi, p.e_split, p.acc_lo, p.acc_hi, p.acc_split, p.partial, p.mode, PASS_BOTH, nullptr))
+        return rc;
+    if (p.n_split_big > p.n_splits)
+        return fail(LGCN_E_ARG, "%s: n_split_big %lld > n_splits %lld", who, (long long)p.n_split_big,
+                    (long long)p.n_splits);
+    out = SpmmArgs{p.items, p.n_items, p.splits, p.n_splits, p.col, p.val, p.x_lo, p.x_hi, p.x_split,
+                   p.e_lo, p.e_hi, p.e_split, p.y, p.acc_lo, p.acc_hi, p.acc_split, p.partial, d, p.mode,
+                   p.div, p.mul, nullptr, nullptr};
+    out.n_big = p.n_split_big < 0 ? -1 : p.n_split_big;
+    return LGCN_OK;
+}
+
 int lgcn_spmm_pair(const lgcn_pass_t* a, const lgcn_pass_t* b, int64_t N, int32_t d, int32_t what,
                    lgcn_stream_t stream) {
     if (!a || !b || what < 1 || what > 3) return fail(LGCN_E_ARG, "lgcn_spmm_pair: bad args");
-    const lgcn_pass_t* ps[2] = {a, b};
     SpmmArgs args[2];
-    for (int i = 0; i < 2; ++i) {
-        const lgcn_pass_t& p = *ps[i];
-        if (int rc = check_pass(p.items, p.n_items, p.splits, p.n_splits, N, d, p.x_lo, p.x_hi, p.x_split, p.e_lo,
-                                p.e_hi, p.e_split, p.acc_lo, p.acc_hi, p.acc_split, p.partial, p.mode, PASS_BOTH,
-                                nullptr))
-            return rc;
-        if (p.n_split_big > p.n_splits)
-            return fail(LGCN_E_ARG, "lgcn_spmm_pair: n_split_big %lld > n_splits %lld", (long long)p.n_split_big,
-                        (long long)p.n_splits);
-        args[i] = SpmmArgs{p.items, p.n_items, p.splits, p.n_splits, p.col, p.val, p.x_lo, p.x_hi, p.x_split,
-                           p.e_lo, p.e_hi, p.e_split, p.y, p.acc_lo, p.acc_hi, p.acc_split, p.partial, d, p.mode,
-                           p.div, p.mul, nullptr, nullptr};
-        args[i].n_big = p.n_split_big < 0 ? -1 : p.n_split_big;
-    }
+    if (int rc = pass_args(*a, N, d, "lgcn_spmm_pair", args[0])) return rc;
+    if (int rc = pass_args(*b, N, d, "lgcn_spmm_pair", args[1])) return rc;
     if (N == 0) return LGCN_OK;
     return dispatch(args[0], N, as_stream(stream), what, nullptr, &args[1]);
+}
+
+int lgcn_spmm_pass(const lgcn_pass_t* p, int64_t N, int32_t d, int32_t what, lgcn_stream_t stream) {
+    if (!p || what < 1 || what > 3) return fail(LGCN_E_ARG, "lgcn_spmm_pass: bad args");
+    SpmmArgs a;
+    if (int rc = pass_args(*p, N, d, "lgcn_spmm_pass", a)) return rc;
+    if (N == 0) return LGCN_OK;
+    return dispatch(a, N, as_stream(stream), what, nullptr, nullptr);
 }
 
 int lgcn_stack_mean_rows(const float* e, const float* const* ys, int32_t K, int64_t rows, int32_t d, float* out,

@@ -68,6 +68,7 @@ _SIGS = {
                               _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp],
                              ctypes.c_int),
     "lgcn_spmm_pair": ([_vp, _vp, _i64, _i32, _i32, _vp], ctypes.c_int),
+    "lgcn_spmm_pass": ([_vp, _i64, _i32, _i32, _vp], ctypes.c_int),
     "lgcn_stack_mean_rows": ([_vp, _vp, _i32, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_scale": ([_vp, _vp, _i64, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_copy_scale": ([_vp, _vp, _i64, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),
@@ -134,7 +135,7 @@ class AdamTensor(ctypes.Structure):
 
 
 class Pass(ctypes.Structure):
-    """lgcn_pass_t: one lgcn_spmm pass's arguments (lgcn_spmm_pair)."""
+    """lgcn_pass_t: one lgcn_spmm pass's arguments (lgcn_spmm_pair, lgcn_spmm_pass)."""
     _fields_ = [("items", ctypes.c_void_p), ("n_items", ctypes.c_int64), ("splits", ctypes.c_void_p),
                 ("n_splits", ctypes.c_int64), ("col", ctypes.c_void_p), ("val", ctypes.c_void_p),
                 ("x_lo", ctypes.c_void_p), ("x_hi", ctypes.c_void_p), ("x_split", ctypes.c_int64),

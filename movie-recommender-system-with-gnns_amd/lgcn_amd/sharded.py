@@ -599,18 +599,30 @@ class ReducePlan:
         return self.scratch.get(key)
 
     # the three kinds of pass; tables are (lo, hi, split = U) split tables
-    def run_partial(self, x_users: torch.Tensor, part_items: torch.Tensor) -> None:
-        from .propagate import spmm
+    def _pass(self, direction, x, e, y, acc, mode: int, div: float, mul: float):
+        """direction's lgcn_pass_t (its split rows combined packed: pack_split_rows' n_split_big)."""
+        N, d = self.shards.N, self.d
+        el, eh, es = e if e is not None else (None, None, N)
+        return _ffi.Pass(direction.items.data_ptr(), direction.n_items, direction.splits.data_ptr(),
+                         direction.n_splits, direction.col.data_ptr(), direction.val.data_ptr(),
+                         _ffi.ptr(x[0]), _ffi.ptr(x[1]), x[2], _ffi.ptr(el), _ffi.ptr(eh), es, _ffi.ptr(y),
+                         _ffi.ptr(acc[0]), _ffi.ptr(acc[1]), acc[2], _ffi.ptr(self._part(direction, d)), mode, div,
+                         mul, n_split_big=getattr(direction, "n_split_big", -1))
 
-        N, U = self.shards.N, self.shards.U
-        spmm(self.partial, N, self.d, (x_users, part_items, U), None, (part_items, part_items, U), None,
-             _ffi.EPI_STORE, 1.0, 1.0, self._part(self.partial, self.d))
+    def _run(self, p, dev) -> None:
+        import ctypes
+
+        _ffi.check(_ffi.load().lgcn_spmm_pass(ctypes.byref(p), self.shards.N, self.d, 3, _ffi.stream_of(dev)),
+                   "lgcn_spmm_pass")
+
+    def run_partial(self, x_users: torch.Tensor, part_items: torch.Tensor) -> None:
+        U = self.shards.U
+        self._run(self._pass(self.partial, (x_users, part_items, U), None, None, (part_items, part_items, U),
+                             _ffi.EPI_STORE, 1.0, 1.0), x_users.device)
 
     def run_users(self, x_items: torch.Tensor, e, acc, y, mode: int, div: float, mul: float) -> None:
-        from .propagate import spmm
-
-        N, U = self.shards.N, self.shards.U
-        spmm(self.users, N, self.d, (x_items, x_items, U), e, acc, y, mode, div, mul, self._part(self.users, self.d))
+        U = self.shards.U
+        self._run(self._pass(self.users, (x_items, x_items, U), e, y, acc, mode, div, mul), x_items.device)
 
     def run_pair(self, x_users: torch.Tensor, part_items: torch.Tensor, x_items: torch.Tensor, e, acc, y, mode: int,
                  div: float, mul: float) -> None:
@@ -618,23 +630,12 @@ class ReducePlan:
         in one, both combines in the other) — the same per-row arithmetic."""
         import ctypes
 
-        N, U, d = self.shards.N, self.shards.U, self.d
-        lib = _ffi.load()
-        el, eh, es = e if e is not None else (None, None, N)
-
-        def pass_of(direction, x, ee, y_, a_lo, a_hi, a_split, m, dv, ml):
-            part = self._part(direction, d)
-            return _ffi.Pass(direction.items.data_ptr(), direction.n_items, direction.splits.data_ptr(),
-                             direction.n_splits, direction.col.data_ptr(), direction.val.data_ptr(),
-                             _ffi.ptr(x[0]), _ffi.ptr(x[1]), x[2], _ffi.ptr(ee[0]), _ffi.ptr(ee[1]), ee[2],
-                             _ffi.ptr(y_), _ffi.ptr(a_lo), _ffi.ptr(a_hi), a_split, _ffi.ptr(part), m, dv, ml,
-                             n_split_big=getattr(direction, "n_split_big", -1))
-
-        pa = pass_of(self.partial, (x_users, part_items, U), (None, None, N), None, part_items, part_items, U,
-                     _ffi.EPI_STORE, 1.0, 1.0)
-        pb = pass_of(self.users, (x_items, x_items, U), (el, eh, es), y, acc[0], acc[1], acc[2], mode, div, mul)
-        _ffi.check(lib.lgcn_spmm_pair(ctypes.byref(pa), ctypes.byref(pb), N, d, 3, _ffi.stream_of(x_users.device)),
-                   "lgcn_spmm_pair")
+        U = self.shards.U
+        pa = self._pass(self.partial, (x_users, part_items, U), None, None, (part_items, part_items, U),
+                        _ffi.EPI_STORE, 1.0, 1.0)
+        pb = self._pass(self.users, (x_items, x_items, U), e, y, acc, mode, div, mul)
+        _ffi.check(_ffi.load().lgcn_spmm_pair(ctypes.byref(pa), ctypes.byref(pb), self.shards.N, self.d, 3,
+                                              _ffi.stream_of(x_users.device)), "lgcn_spmm_pair")
 
     def finish_items(self, x0i: torch.Tensor, layers: list, last_share: torch.Tensor, out_i: torch.Tensor,
                      div: float, mul: float) -> None:

@@ -205,3 +205,44 @@ def test_adam_consts_are_the_checked_schedule(gpu):
     assert np.array_equal(c[1:, 0].view(np.uint32), host_s.view(np.uint32))
     _ffi.check(lib.lgcn_adam_consts(consts.data_ptr(), 1, 10, 1e-3, 0.9, float(np.float32(0.999)), s), "consts")
     assert float(consts[0, 0].item()) == 0.0
+
+
+@pytest.mark.parametrize("d", [4, 8, 16, 32, 64, 128, 256, 512, 6])
+@pytest.mark.parametrize("chunk,packed", [(8, False), (8, True), (2, True), (4096, True)])
+def test_spmm_pass_bitwise_spmm(gpu, d, chunk, packed):
+    """lgcn_spmm_pass (one plain pass from an lgcn_pass_t; packed: the <= 16-chunk split rows
+    combined one per lane group, pack_split_rows' order) is bitwise lgcn_spmm on the same rows —
+    for every epilogue mode the reduce-mode forward uses, at vector widths and a scalar one (d=6)."""
+    import graphs
+
+    from lgcn_amd import _ffi
+    from lgcn_amd.plan import pack_split_rows
+    from lgcn_amd.propagate import spmm
+
+    U, I, ei = graphs.hub(U=1500, I=40, seed=1)
+    N = U + I
+    da = _direction(gpu, ei, N, chunk, U)
+    if packed:
+        pack_split_rows(da)
+    if chunk == 2:
+        assert da.n_split_big > 0 and da.n_splits > da.n_split_big
+    g = torch.Generator(device=gpu).manual_seed(d + chunk)
+    x = torch.randn(N, d, device=gpu, generator=g)
+    e = torch.randn(N, d, device=gpu, generator=g)
+    part = torch.empty((max(1, da.n_partials), d), device=gpu)
+    lib = _ffi.load()
+    for mode in (_ffi.EPI_STORE, _ffi.EPI_INIT, _ffi.EPI_ADD, _ffi.EPI_FINAL_ACC):
+        ee = (e, None, N) if mode == _ffi.EPI_INIT else None
+        outs = []
+        for how in ("spmm", "pass", "pass"):  # twice: nothing carried between launches
+            acc = torch.full((N, d), 0.5, device=gpu)
+            y = torch.zeros(N, d, device=gpu)
+            if how == "spmm":
+                spmm(da, N, d, (x, None, N), ee, (acc, None, N), y, mode, 4.0, 1.0, part)
+            else:
+                p = _pass(da, x, y, acc, part, mode, e=e if ee else None, div=4.0, packed=packed)
+                _ffi.check(lib.lgcn_spmm_pass(ctypes.byref(p), N, d, 3, _ffi.stream_of(gpu)), "pass")
+            torch.cuda.synchronize()
+            outs.append((acc.cpu(), y.cpu()))
+        for got in outs[1:]:
+            assert torch.equal(got[0], outs[0][0]) and torch.equal(got[1], outs[0][1]), mode

@@ -2,7 +2,9 @@
 ReducePlan: users sharded, item partials all-reduced) on one GPU, per R x F grid, without the
 all_reduce (a stand-in reducer that moves nothing): the time a rank spends in its kernels per K=3
 step, next to the bytes a ring all_reduce of its item partials moves per rank.
-python tools/reduce_rank_probe.py [--grids 2x1,4x1,8x1,2x2,4x2,2x4] [--orders overlapped,fused,fused-seq]"""
+python tools/reduce_rank_probe.py [--grids 2x1,4x1,8x1,2x2,4x2,2x4] [--orders overlapped,fused,fused-seq]
+An order suffixed -u (overlapped-u, fused-u) combines every split row with a workgroup of its own
+(n_split_big = -1) instead of packing the <= 16-chunk ones one per lane group."""
 import argparse
 import os
 import sys
@@ -64,6 +66,12 @@ def main():
             red = NoReduce(R)
             for order in times:
                 fused = order.startswith("fused")
+                unpacked = order.endswith("-u")
+                nb = {}
+                for dr in (rplan.users, rplan.partial):
+                    nb[id(dr)] = dr.n_split_big
+                    if unpacked:
+                        dr.n_split_big = -1
                 # fused-seq: the pair launch without its XCD-split block mapping (LGCN_PAIR_XCD=0);
                 # fusedN: pass a (the item partials) on N of the 8 XCDs
                 os.environ["LGCN_PAIR_XCD"] = ("0" if order == "fused-seq" else
@@ -78,6 +86,8 @@ def main():
                         propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)
                     torch.cuda.synchronize()
                 times[order].append((time.perf_counter() - t) / args.steps * 1e3)
+                for dr in (rplan.users, rplan.partial):
+                    dr.n_split_big = nb[id(dr)]
                 moved = red.bytes / args.steps
             del rplan
         for order, ts in times.items():
