@@ -3,6 +3,8 @@ ReducePlan: users sharded, item partials all-reduced) on one GPU, per R x F grid
 all_reduce (a stand-in reducer that moves nothing): the time a rank spends in its kernels per K=3
 step, next to the bytes a ring all_reduce of its item partials moves per rank.
 python tools/reduce_rank_probe.py [--grids 2x1,4x1,8x1,2x2,4x2,2x4] [--orders overlapped,fused,fused-seq]
+A +g suffix (fused+g, ...) captures the step in a hipGraph once and times its replays (no host
+launch overhead).
 An order suffixed -u (overlapped-u, fused-u) combines every split row with a workgroup of its own
 (n_split_big = -1) instead of packing the <= 16-chunk ones one per lane group."""
 import argparse
@@ -64,9 +66,12 @@ def main():
             rplan = ReducePlan(ei, shards, gr, c1 - c0, args.chunk)
             x0u, x0i = uw[:, c0:c1].contiguous(), iw[:, c0:c1].contiguous()
             red = NoReduce(R)
+            moved_per_step = 0
             for order in times:
-                fused = order.startswith("fused")
-                unpacked = order.endswith("-u")
+                graph = order.endswith("+g")
+                base = order[:-2] if graph else order
+                fused = base.startswith("fused")
+                unpacked = base.endswith("-u")
                 nb = {}
                 for dr in (rplan.users, rplan.partial):
                     nb[id(dr)] = dr.n_split_big
@@ -81,10 +86,25 @@ def main():
                         propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)
                     torch.cuda.synchronize()
                     red.bytes = 0
-                    t = time.perf_counter()
-                    for _ in range(args.steps):
-                        propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)
-                    torch.cuda.synchronize()
+                    if graph:  # the step captured once, replayed: the GPU side without host overhead
+                        cg = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(cg):
+                            propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)
+                        cg.replay()
+                        torch.cuda.synchronize()
+                        red.bytes = 0
+                        t = time.perf_counter()
+                        for _ in range(args.steps):
+                            cg.replay()
+                            red.bytes += moved_per_step
+                        torch.cuda.synchronize()
+                        del cg
+                    else:
+                        t = time.perf_counter()
+                        for _ in range(args.steps):
+                            propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)
+                        torch.cuda.synchronize()
+                        moved_per_step = red.bytes / args.steps
                 times[order].append((time.perf_counter() - t) / args.steps * 1e3)
                 for dr in (rplan.users, rplan.partial):
                     dr.n_split_big = nb[id(dr)]
