@@ -658,8 +658,12 @@ def main():
         if sharded:
             workload += f"_grid{grid.R}x{grid.F}"
     sliced = isinstance(scheds[0], SlicedDirection)
+    riding = sliced and K > 1 and os.environ.get("LGCN_SLICE_RIDE", "1") != "0" and bool(getattr(scheds[0], "_ride", None))
     kernel_name = (f"k_spmm_vec<{kernel_lpr(d)},sliced> (lgcn_spmm_run_slices, {launches} source-slice "
                    f"launches per layer)" if sliced else f"k_spmm_vec<{kernel_lpr(d)}> (lgcn_spmm_items)")
+    if riding:
+        kernel_name = (f"k_spmm_vec / k_spmm_ride<{kernel_lpr(d)},sliced> (lgcn_spmm_run_slices_ride, {launches} "
+                       f"source-slice launches per layer, two of them carrying the split-row combine)")
     graph_stats = (graph.degree_stats() if graph is not None else {"num_nodes": N, "num_edges": E})
     signature = traffic_signature(workload, kernel_name, launches, items_mine, e_mine, graph_stats)
     traffic, stale = load_traffic(signature)

@@ -308,6 +308,24 @@ int lgcn_spmm_pair(const lgcn_pass_t* a, const lgcn_pass_t* b, int64_t N, int32_
  * overlapped order runs its passes one at a time through this (ABI 5). Any d lgcn_spmm takes. */
 int lgcn_spmm_pass(const lgcn_pass_t* p, int64_t N, int32_t d, int32_t what, lgcn_stream_t stream);
 
+/* lgcn_spmm_run_slices with a riding combine (ABI 5): the split rows of `ride` (an lgcn_pass_t of
+ * which only splits / n_splits / n_split_big / partial / e / y / acc / mode / div / mul are used,
+ * its x tables must be non-NULL) are combined by extra workgroups of slice launch `ride_slice`
+ * instead of by a launch of their own (an empty ride slice: a combine launch of its own). The
+ * caller guarantees that slice launch neither reads nor writes the ride's rows, its partial slots
+ * or its y rows. The one-GPU K-layer forward (lgcn_amd.propagate) alternates its two slice groups
+ * per layer — user-table slices (which write item rows) and item-table slices (which write user
+ * rows) — so each group's split rows ride in the next group's first launch, reading partials from
+ * a buffer the next layer does not write: one combine launch per forward instead of one per layer.
+ * Per row the same arithmetic as lgcn_spmm_run_slices + lgcn_spmm_combine (bitwise). Vector widths
+ * only (d in {4, 8, ..., 1024}, 16-byte aligned rows). Same reference code as lgcn_spmm. */
+int lgcn_spmm_run_slices_ride(const lgcn_item_t* items, const int64_t* slice_offsets, int32_t S, const int32_t* col,
+                              const float* val, int64_t N, int32_t d, const float* x_lo, const float* x_hi,
+                              int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split, float* y,
+                              float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
+                              float div, float mul, lgcn_stream_t stream, float* run, const lgcn_pass_t* ride,
+                              int32_t ride_slice);
+
 /* The layer-stack mean of rows whose layer outputs were kept instead of accumulated (ABI 5):
  * out[r] = ((((e[r] + y_0[r]) + y_1[r]) + ... + y_{K-1}[r]) / div) * mul for r in [0, rows) — the
  * additions and roundings of the INIT, ADD..., FINAL_ACC epilogue sequence (K == 1: FINAL_E), so

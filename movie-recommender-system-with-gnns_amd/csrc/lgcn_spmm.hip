@@ -539,6 +539,20 @@ __global__ __launch_bounds__(kBlock) void k_combine_packed(SpmmArgs a) {
     combine_block<LPR, NV>(a, blockIdx.x);
 }
 
+// One source-slice launch of a sliced schedule (a, SLICED item pass) carrying another pass's split
+// rows (r: combine only) as its first rb workgroups (lgcn_spmm_run_slices_ride): the combine of one
+// side's split rows of the layer before, or of the other slice group of this layer, rides in a
+// launch that neither reads nor writes those rows or their partials, instead of a launch of its own.
+template <int LPR, int NV, int UNROLL, int TAIL, int CM>
+__global__ __launch_bounds__(kBlock) void k_spmm_ride(SpmmArgs a, SpmmArgs r, int64_t rb) {
+    const int64_t blk = blockIdx.x;
+    if (blk < rb) {
+        combine_block<LPR, NV>(r, blk);
+        return;
+    }
+    item_pass<LPR, NV, UNROLL, true, TAIL, false, CM>(a, blk - rb);
+}
+
 // The split rows of two passes in one launch: a's workgroups first, then b's.
 template <int LPR, int NV>
 __global__ __launch_bounds__(kBlock) void k_combine_pair(SpmmArgs a, SpmmArgs b, int64_t blocks_a) {
@@ -621,11 +635,19 @@ __global__ __launch_bounds__(kBlock) void k_combine_scalar(SpmmArgs a) {
     finish_row_scalar(a, sp.row, l, acc);
 }
 
-enum { PASS_ITEMS = 1, PASS_COMBINE = 2, PASS_BOTH = 3, PASS_BSPLIT = 4 };
+enum { PASS_ITEMS = 1, PASS_COMBINE = 2, PASS_BOTH = 3, PASS_BSPLIT = 4, PASS_RIDE = 8 };
 
 template <int LPR, int NV, int UNROLL, int TAIL = 0, int CM = 1>
 int launch_vec(const SpmmArgs& a, hipStream_t s, int pass, const SpmmArgs* b = nullptr) {
     constexpr int GPB = kBlock / LPR;
+    if (pass == PASS_RIDE) {  // lgcn_spmm_run_slices_ride: a's slice items + b's split-row combine
+        const int64_t blocks = (a.n_items + GPB - 1) / GPB, rb = b->n_splits > 0 ? combine_blocks<LPR, NV>(*b) : 0;
+        if (blocks + rb > 0) {
+            k_spmm_ride<LPR, NV, UNROLL, TAIL, CM><<<dim3(static_cast<unsigned>(blocks + rb)), kBlock, 0, s>>>(a, *b, rb);
+            return check_launch("k_spmm_ride");
+        }
+        return LGCN_OK;
+    }
     if (b != nullptr) {  // lgcn_spmm_pair: two plain passes, one launch per half
         if (pass & PASS_ITEMS) {
             const int64_t ba = (a.n_items + GPB - 1) / GPB, bb = (b->n_items + GPB - 1) / GPB;
@@ -798,12 +820,14 @@ int dispatch(SpmmArgs& a, int64_t N, hipStream_t s, int pass, float* run, const 
     SpmmArgs bb;
     if (b != nullptr) {
         bb = *b;
-        bb.nt = a.nt;
+        bb.nt = pass == PASS_RIDE ? 0 : a.nt;  // a riding combine keeps the standalone combine's stores
         b = &bb;
     }
 
     const bool vec_ok = vec_aligned(a) && (b == nullptr || vec_aligned(*b));
-    if (b != nullptr && !vec_ok) return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm_pair: needs d in {4,8,...,1024} and aligned rows");
+    if (b != nullptr && !vec_ok)
+        return fail(LGCN_E_UNSUPPORTED, "%s: needs d in {4,8,...,1024} and aligned rows",
+                    pass == PASS_RIDE ? "lgcn_spmm_run_slices_ride" : "lgcn_spmm_pair");
     if (vec_ok) {
         // Predicated tail (TAIL = 1): a row's last < UNROLL edges of each batch are gathered
         // together instead of one at a time. It costs VGPRs (occupancy 6-7 -> 4 waves/SIMD at
@@ -946,6 +970,46 @@ int lgcn_spmm_pass(const lgcn_pass_t* p, int64_t N, int32_t d, int32_t what, lgc
     if (int rc = pass_args(*p, N, d, "lgcn_spmm_pass", a)) return rc;
     if (N == 0) return LGCN_OK;
     return dispatch(a, N, as_stream(stream), what, nullptr, nullptr);
+}
+
+int lgcn_spmm_run_slices_ride(const lgcn_item_t* items, const int64_t* slice_offsets, int32_t S, const int32_t* col,
+                              const float* val, int64_t N, int32_t d, const float* x_lo, const float* x_hi,
+                              int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split, float* y,
+                              float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
+                              float div, float mul, lgcn_stream_t stream, float* run, const lgcn_pass_t* ride,
+                              int32_t ride_slice) {
+    if (!run || S < 0 || (S > 0 && (!items || !slice_offsets)))
+        return fail(LGCN_E_ARG, "lgcn_spmm_run_slices_ride: bad args");
+    SpmmArgs r{};
+    const bool riding = ride != nullptr && ride->n_splits > 0;
+    if (riding) {
+        if (ride_slice < 0 || ride_slice >= S)
+            return fail(LGCN_E_ARG, "lgcn_spmm_run_slices_ride: ride_slice %d outside [0, %d)", ride_slice, S);
+        if (int rc = pass_args(*ride, N, d, "lgcn_spmm_run_slices_ride", r)) return rc;
+    }
+    for (int32_t sl = 0; sl < S; ++sl) {
+        const int64_t b = slice_offsets[sl], n = slice_offsets[sl + 1] - b;
+        if (b < 0 || n < 0) return fail(LGCN_E_ARG, "lgcn_spmm_run_slices_ride: offsets not ascending at slice %d", sl);
+        const bool here = riding && sl == ride_slice;
+        if (here && n == 0) {  // nothing to ride in: the combine alone
+            if (int rc = dispatch(r, N, as_stream(stream), PASS_COMBINE, nullptr, nullptr)) return rc;
+            continue;
+        }
+        if (n == 0) continue;
+        if (!here) {
+            if (int rc = spmm_impl(items + b, n, nullptr, 0, col, val, N, d, x_lo, x_hi, x_split, e_lo, e_hi, e_split,
+                                   y, acc_lo, acc_hi, acc_split, partial, mode, div, mul, stream, PASS_ITEMS, run))
+                return rc;
+            continue;
+        }
+        if (int rc = check_pass(items + b, n, nullptr, 0, N, d, x_lo, x_hi, x_split, e_lo, e_hi, e_split, acc_lo,
+                                acc_hi, acc_split, partial, mode, PASS_ITEMS, nullptr))
+            return rc;
+        SpmmArgs a{items + b, n, nullptr, 0, col, val, x_lo, x_hi, x_split, e_lo, e_hi, e_split,
+                   y, acc_lo, acc_hi, acc_split, partial, d, mode, div, mul, run, nullptr};
+        if (int rc = dispatch(a, N, as_stream(stream), PASS_RIDE, run, &r)) return rc;
+    }
+    return LGCN_OK;
 }
 
 int lgcn_stack_mean_rows(const float* e, const float* const* ys, int32_t K, int64_t rows, int32_t d, float* out,

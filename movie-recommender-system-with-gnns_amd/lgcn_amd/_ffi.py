@@ -64,6 +64,10 @@ _SIGS = {
     "lgcn_spmm_run_slices": ([_vp, _vp, _i32, _vp, _vp, _i64, _i32,
                               _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp],
                              ctypes.c_int),
+    "lgcn_spmm_run_slices_ride": ([_vp, _vp, _i32, _vp, _vp, _i64, _i32,
+                                   _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp,
+                                   _vp, _i32],
+                                  ctypes.c_int),
     "lgcn_spmm_blocksplit": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
                               _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp],
                              ctypes.c_int),

@@ -11,6 +11,8 @@ No intermediate x_k is saved: Â is linear, so the backward needs only the plan 
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -121,6 +123,13 @@ def propagate_forward(user_w: torch.Tensor, item_w: torch.Tensor, plan: Propagat
                    "lgcn_copy_scale")
         return out
     f = plan.schedule("fwd", d)
+    if (K > 1 and isinstance(f, SlicedDirection) and os.environ.get("LGCN_SLICE_RIDE", "1") != "0"
+            and d % 4 == 0 and d <= 1024 and (d & (d - 1)) == 0):
+        from .sliced import ride_layout
+
+        if ride_layout(f, U) is not None:
+            _forward_sliced_ride(f, N, U, d, x0, acc, K, div, mul, stream)
+            return out
     partial = torch.empty((f.n_partials, d), dtype=torch.float32, device=dev) if f.n_partials else None
     if K == 1:
         spmm(f, N, d, x0, x0, acc, None, _ffi.EPI_FINAL_E, div, mul, partial, stream)
@@ -134,6 +143,78 @@ def propagate_forward(user_w: torch.Tensor, item_w: torch.Tensor, plan: Propagat
     last = bufs[(K - 2) % len(bufs)]
     spmm(f, N, d, (last, None, N), None, acc, None, _ffi.EPI_FINAL_ACC, div, mul, partial, stream)
     return out
+
+
+def _forward_sliced_ride(f, N: int, U: int, d: int, x0, acc, K: int, div: float, mul: float, stream: int) -> None:
+    """propagate_forward over a sliced schedule with riding combines (K >= 2). Per layer the two
+    slice groups run one after the other — user-table slices (writing item rows) and item-table
+    slices (writing user rows), the group order alternating from layer to layer — and the split
+    rows a group wrote are combined by extra workgroups of the NEXT group's first launch
+    (lgcn_spmm_run_slices_ride): that launch gathers the other table of its layer and writes the
+    other side's rows, so it never touches the rows, y or partial slots being combined. Partials
+    alternate between two buffers by layer parity (a layer's first group writes the partial slots
+    that the previous layer's split rows are being read from). The last group's split rows get a
+    combine launch of their own. Each row: the slice launches and combine of propagate_forward,
+    in the same order — bitwise its result."""
+    import ctypes
+
+    lib = _ffi.load()
+    dev = acc[0].device
+    r = f._ride
+    S = len(f.launches)
+    groups = {"u": (0, r["nu"]), "i": (r["nu"], S)}
+    writes = {"u": "items", "i": "users"}
+    parts = [torch.empty((f.n_partials, d), dtype=torch.float32, device=dev) if f.n_partials else None
+             for _ in range(2)]
+    bufs = [torch.empty((N, d), dtype=torch.float32, device=dev) for _ in range(min(2, K - 1))]
+    scratch = torch.empty((N, d), dtype=torch.float32, device=dev)  # the last layer's running sums
+    al, ah, as_ = acc
+    offs = ctypes.addressof(f.host_offsets)
+
+    def layer(k):
+        if k == 1:
+            return dict(x=x0, e=x0, y=bufs[0], mode=_ffi.EPI_INIT, div=1.0, mul=1.0, part=parts[1])
+        x = (bufs[(k - 2) % len(bufs)], None, N)
+        if k < K:
+            return dict(x=x, e=None, y=bufs[(k - 1) % len(bufs)], mode=_ffi.EPI_ADD, div=1.0, mul=1.0,
+                        part=parts[k % 2])
+        return dict(x=x, e=None, y=None, mode=_ffi.EPI_FINAL_ACC, div=div, mul=mul, part=parts[k % 2])
+
+    def ride_pass(side, lay):
+        beg, n, nb = r[side]
+        if n == 0:
+            return None
+        xl, xh, xs = lay["x"]
+        el, eh, es = lay["e"] if lay["e"] is not None else (None, None, N)
+        return _ffi.Pass(None, 0, f.splits.data_ptr() + 16 * beg, n, _ffi.ptr(f.base.col), _ffi.ptr(f.base.val),
+                         _ffi.ptr(xl), _ffi.ptr(xh), xs, _ffi.ptr(el), _ffi.ptr(eh), es, _ffi.ptr(lay["y"]),
+                         _ffi.ptr(al), _ffi.ptr(ah), as_, _ffi.ptr(lay["part"]), lay["mode"], lay["div"], lay["mul"],
+                         n_split_big=nb)
+
+    pending = None  # the split rows of the last group issued, with their layer's arguments
+    for k in range(1, K + 1):
+        lay = layer(k)
+        xl, xh, xs = lay["x"]
+        el, eh, es = lay["e"] if lay["e"] is not None else (None, None, N)
+        run = lay["y"] if lay["y"] is not None else scratch
+        for grp in (("u", "i") if k % 2 == 1 else ("i", "u")):
+            a, b = groups[grp]
+            ride = ride_pass(*pending) if pending is not None else None
+            args = (f.items.data_ptr(), ctypes.c_void_p(offs + 8 * a), b - a, _ffi.ptr(f.base.col),
+                    _ffi.ptr(f.base.val), N, d, _ffi.ptr(xl), _ffi.ptr(xh), xs, _ffi.ptr(el), _ffi.ptr(eh), es,
+                    _ffi.ptr(lay["y"]), _ffi.ptr(al), _ffi.ptr(ah), as_, _ffi.ptr(lay["part"]), lay["mode"],
+                    lay["div"], lay["mul"], stream, run.data_ptr(),
+                    ctypes.byref(ride) if ride is not None else None, 0)
+            if _launch_timer is not None:
+                with _launch_timer(d, sum(1 for _, n in f.launches[a:b] if n)):
+                    rc = lib.lgcn_spmm_run_slices_ride(*args)
+            else:
+                rc = lib.lgcn_spmm_run_slices_ride(*args)
+            _ffi.check(rc, "lgcn_spmm_run_slices_ride")
+            pending = (writes[grp], lay)
+    ride = ride_pass(*pending)
+    if ride is not None:
+        _ffi.check(lib.lgcn_spmm_pass(ctypes.byref(ride), N, d, 2, stream), "lgcn_spmm_pass (last combine)")
 
 
 def propagate_backward(dout: torch.Tensor, plan: PropagationPlan, U: int, K: int) -> tuple[torch.Tensor, torch.Tensor]:

@@ -59,6 +59,12 @@ def slice_bounds(N: int, U: int, d: int, slice_bytes: int) -> list[int]:
         if n <= 0:
             continue
         k = min(MAX_SLICES // 2, max(1, -(-n * d * 4 // slice_bytes)))
+        if lo == U and U > 0 and n * d * 4 <= 2 * slice_bytes:
+            # an item range of up to two slices stays whole: every user row then gets its sum in one
+            # segment (no running-sum store and reload between item slices). C2 d=64 (15.1 MB at
+            # 8 MB slices): 1.230-1.234 -> 1.224-1.226 ms per K=3 step, 3 interleaved pairs
+            # (profiles/r04u_item_slice/)
+            k = 1
         out += [lo + (n * i) // k for i in range(1, k)] + [hi]
     return sorted(set(out))
 
@@ -135,6 +141,49 @@ def spmm_sliced_combine(sd: SlicedDirection, N: int, d: int, x, e, acc, y, mode:
         lib = _ffi.load()
         tail = _tail(sd, N, d, x, e, acc, y, mode, div, mul, partial, stream)
         _ffi.check(lib.lgcn_spmm_combine(None, 0, sd.splits.data_ptr(), sd.n_splits, *tail), "lgcn_spmm_combine")
+
+
+def _bipartite(rowptr: torch.Tensor, col: torch.Tensor, U: int) -> bool:
+    """Every edge joins a row < U and a row >= U (then user-table slices write only item rows and
+    item-table slices only user rows — what the riding combine relies on)."""
+    N = rowptr.numel() - 1
+    if col.numel() == 0:
+        return True
+    deg = rowptr[1:] - rowptr[:-1]
+    dst_user = torch.repeat_interleave(torch.arange(N, device=col.device) < U, deg)
+    return bool(((col < U) != dst_user).all().item())
+
+
+def ride_layout(sd: SlicedDirection, U: int) -> dict | None:
+    """Prepare sd for the riding combine of the K-layer forward (lgcn_spmm_run_slices_ride): its
+    split rows ordered users first, then items, each side big-first (<= 16-chunk rows packed one
+    per lane group), and the slice groups: slices [0, nu) gather user rows (they write item rows),
+    [nu, S) gather item rows (they write user rows). None when the bounds do not separate the two
+    tables (one group: nothing to ride in). One host read-back per plan."""
+    r = getattr(sd, "_ride", None)
+    if r is not None:
+        return r or None
+    S = len(sd.launches)
+    nu = sd.bounds.index(U) if U in sd.bounds else -1
+    base = sd.base
+    if nu <= 0 or nu >= S or not _bipartite(base.rowptr, base.col, U):
+        sd._ride = {}
+        return None
+    from .plan import SMALL_SPLIT_CHUNKS
+
+    n = sd.n_splits
+    counts = (0, 0, 0, 0)
+    if n:
+        sp = sd.splits[:n]
+        side = (sp[:, 0] >= U).to(torch.int64)
+        small = (sp[:, 2] <= SMALL_SPLIT_CHUNKS).to(torch.int64)
+        key = side * 2 + small
+        order = torch.argsort(key, stable=True)
+        sd.splits[:n] = sp[order].clone()
+        counts = tuple(int(v) for v in torch.bincount(key, minlength=4).cpu().tolist())
+    n_users = counts[0] + counts[1]
+    sd._ride = {"nu": nu, "users": (0, n_users, counts[0]), "items": (n_users, counts[2] + counts[3], counts[2])}
+    return sd._ride
 
 
 def propagate_forward_sliced(user_w: torch.Tensor, item_w: torch.Tensor, sd: SlicedDirection, K: int) -> torch.Tensor:

@@ -171,3 +171,53 @@ def test_index_rounds_bitwise(gpu, force_slices, monkeypatch, d, cms, sliced):
         assert np.array_equal(o, outs[0])
     _, w = c_oracle.gcn_norm(ei, N)
     assert_rows_close(outs[0], c_oracle.lgconv(x.cpu().numpy(), ei, w))
+
+
+@pytest.mark.parametrize("name", ["sym", "subsampled", "hub"])
+@pytest.mark.parametrize("K,d,mb", [(2, 64, 0.005), (3, 64, 0.01), (4, 16, 0.002), (5, 128, 0.02), (3, 256, 0.05)])
+def test_sliced_ride_bitwise(gpu, force_slices, monkeypatch, name, K, d, mb):
+    """The riding-combine forward (lgcn_spmm_run_slices_ride: slice groups alternating per layer,
+    each group's split rows combined inside the next group's first launch, partials double-buffered
+    by layer parity, one combine launch at the end) is bitwise the per-layer slices + combine — run
+    twice to show nothing carries over between calls."""
+    from lgcn_amd import propagate_forward
+    from lgcn_amd.sliced import ride_layout
+
+    U, I, ei = graphs.ALL[name]()
+    N = U + I
+    force_slices(mb)
+    plan = _plan(ei, N, gpu, U, chunk=8)
+    sched = plan.schedule("fwd", d)
+    r = ride_layout(sched, U)
+    assert r is not None and 0 < r["nu"] < len(sched.launches)
+    assert r["users"][1] + r["items"][1] == sched.n_splits
+    uw, iw = graphs.embeddings(U, I, d, seed=K + d)
+    uw_t, iw_t = torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu)
+    monkeypatch.setenv("LGCN_SLICE_RIDE", "0")
+    want = propagate_forward(uw_t, iw_t, plan, K).cpu()
+    monkeypatch.setenv("LGCN_SLICE_RIDE", "1")
+    for _ in range(2):
+        got = propagate_forward(uw_t, iw_t, plan, K).cpu()
+        assert torch.equal(got, want)
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
+    assert_rows_close(got.numpy(), np.concatenate([ru, ri]))
+
+
+def test_sliced_ride_off_for_non_bipartite(gpu, force_slices):
+    """A user-user edge breaks the two groups' disjointness: no riding layout, and the forward
+    (per-layer combines) still matches the oracle."""
+    from lgcn_amd import propagate_forward
+    from lgcn_amd.sliced import SlicedDirection, ride_layout
+
+    U, I, ei = graphs.sym()
+    ei = np.concatenate([ei, np.array([[1, 2], [2, 1]], dtype=ei.dtype)], axis=1)
+    ei = np.ascontiguousarray(ei[:, np.lexsort((ei[0], ei[1]))])  # coalesced: the sliced schedule needs it
+    N, d, K = U + I, 64, 3
+    force_slices(0.005)
+    plan = _plan(ei, N, gpu, U, chunk=8)
+    sched = plan.schedule("fwd", d)
+    assert isinstance(sched, SlicedDirection) and ride_layout(sched, U) is None
+    uw, iw = graphs.embeddings(U, I, d, seed=1)
+    out = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, K).cpu().numpy()
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
+    assert_rows_close(out, np.concatenate([ru, ri]))

@@ -2,7 +2,7 @@
 profiles/pmc_traffic.json: average memory-side bytes per k_spmm_vec launch =
 FETCH_SIZE x calibration (tools/calib_fetch.py: a permutation gather that must read every byte
 once) + WRITE_SIZE, each from its own --pmc pass.
-python tools/pmc_to_traffic.py <profile dir> <workload key> [--kernel k_spmm_vec]"""
+python tools/pmc_to_traffic.py <profile dir> <workload key> [--kernel k_spmm_vec,k_spmm_ride]"""
 import argparse
 import csv
 import glob
@@ -17,7 +17,7 @@ def per_launch(path, counter, kernel):
     vals = {}
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if any(k in r["Kernel_Name"] for k in kernel.split(",")) and r["Counter_Name"] == counter:
                 vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return list(vals.values())
 
@@ -26,7 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof")
     ap.add_argument("workload")
-    ap.add_argument("--kernel", default="k_spmm_vec")
+    # the item pass: plain slice launches and the ones carrying a riding combine (comma = any of)
+    ap.add_argument("--kernel", default="k_spmm_vec,k_spmm_ride")
     args = ap.parse_args()
     # FETCH_SIZE / WRITE_SIZE are in KiB on gfx950 (rocprofv3 derived counters)
     fetch = per_launch(os.path.join(args.prof, "pmc_fetch"), "FETCH_SIZE", args.kernel)
