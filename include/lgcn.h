@@ -38,7 +38,7 @@ extern "C" {
 
 typedef void* lgcn_stream_t; /* a hipStream_t; NULL = the null stream */
 
-#define LGCN_ABI_VERSION 5
+#define LGCN_ABI_VERSION 6
 
 #define LGCN_OK 0
 #define LGCN_E_ARG (-1)         /* bad size / null pointer / unsupported argument */
@@ -461,8 +461,9 @@ int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, co
  * Row-lazy Adam (lgcn_rowadam.hip) for the sparse batch step: exact replay of the zero-gradient
  * steps a row missed, when the row is next touched (reference utils/train_test.py:95-96; same
  * element arithmetic as lgcn_adam_step). Tables p/g/m/v are (lo, hi) split at `split` rows of d.
- *   lgcn_adam_consts: consts[t] = (float(-lr / (1 - beta1^t)), float(sqrt(1 - beta2^t))),
- *     t in [t0, t1] (float pairs), the lgcn_adam_prologue formulas; consts[0].x = 1 when beta2 is
+ *   lgcn_adam_consts: consts[t] = (s, c, 1.0f / c, 0) with s = float(-lr / (1 - beta1^t)) and
+ *     c = float(sqrt(1 - beta2^t)), t in [t0, t1] (4 floats per step, 16-byte aligned; ABI 6 — ABI 5
+ *     had (s, c) pairs), the lgcn_adam_prologue formulas; consts[0].x = 1 when beta2 is
  *     exactly 0.999 (the schedule whose step-constant division lgcn_row_adam may take by Markstein's
  *     proven-exact shortcut; set by a call with t0 = 1, cleared by a call with another beta2), else 0.
  *   lgcn_row_adam: rows = rows_a[0..n_a) then keys_b[j] + off_b (j counted only if first_b[j]

@@ -10,7 +10,7 @@
 // every row up to the current step (epoch end / before parameters are read).
 //
 //   last[r]   the last step applied to row r (int32 per global row id)
-//   consts[t] (step_size_t, bc2_sqrt_t), t = 1..T: the per-step constants, filled by
+//   consts[t] (step_size_t, bc2_sqrt_t, 1 / bc2_sqrt_t, 0), t = 1..T: the per-step constants, filled by
 //             lgcn_adam_consts with the same double formulas as lgcn_adam_prologue
 //   step      device int64: the number of completed steps (capturable; lgcn_row_adam_update
 //             advances it)
@@ -125,15 +125,18 @@ __device__ __forceinline__ bool list_row(const RowList& L, int64_t i, int64_t& r
 // cleared by any call with another beta2.
 constexpr double kMarksteinBeta2 = 0.999;
 
-__global__ void k_adam_consts(float2* __restrict__ consts, int64_t t0, int64_t t1, float lr, double beta1,
+__global__ void k_adam_consts(float4* __restrict__ consts, int64_t t0, int64_t t1, float lr, double beta1,
                               double beta2) {
     const int64_t t = t0 + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0 && (t0 == 1 || beta2 != kMarksteinBeta2))
-        consts[0] = make_float2(beta2 == kMarksteinBeta2 ? 1.0f : 0.0f, 0.0f);
+        consts[0] = make_float4(beta2 == kMarksteinBeta2 ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f);
     if (t > t1) return;
     const double bc1 = 1.0 - pow(beta1, double(t));
     const double bc2 = 1.0 - pow(beta2, double(t));
-    consts[t] = make_float2(static_cast<float>(-(static_cast<double>(lr) / bc1)), static_cast<float>(sqrt(bc2)));
+    const float c = static_cast<float>(sqrt(bc2));
+    // z: 1 / c in fp32 (correctly rounded), the reciprocal div_step's shortcut multiplies by —
+    // built once here instead of once per replayed step and lane
+    consts[t] = make_float4(static_cast<float>(-(static_cast<double>(lr) / bc1)), c, 1.0f / c, 0.0f);
 }
 
 // One LPR-lane group per list entry (or per row for the flush). mode 0: catch the row up to
@@ -143,7 +146,7 @@ __global__ void k_adam_consts(float2* __restrict__ consts, int64_t t0, int64_t t
 template <int LPR, int NV>
 __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int64_t n_rows, int32_t* __restrict__ last,
                                                      int32_t* __restrict__ claim, const int64_t* __restrict__ step,
-                                                     const float2* __restrict__ consts, AdamK k,
+                                                     const float4* __restrict__ consts, AdamK k,
                                                      const float* __restrict__ clip, int mode) {
     constexpr int GPB = kBlock / LPR;
     const int g = threadIdx.x / LPR;
@@ -192,8 +195,8 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
         v[q] = V[q * LPR];
     }
     for (int64_t s = from; s <= upto; ++s) {
-        const float2 c = consts[s];
-        const float rc = 1.0f / c.y;  // once per step, shared by the lane's 4 NV elements
+        const float4 c = consts[s];
+        const float rc = c.z;  // 1 / c.y, from lgcn_adam_consts
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             adam_elem_zero(p[q].x, m[q].x, v[q].x, c.x, c.y, rc, k);
@@ -204,8 +207,8 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
     }
     int32_t now = static_cast<int32_t>(upto);
     if (upd) {
-        const float2 c = consts[t + 1];
-        const float rc = 1.0f / c.y;
+        const float4 c = consts[t + 1];
+        const float rc = c.z;
         const float4* G = reinterpret_cast<const float4*>(trow(T.g_lo, T.g_hi, T.split, row, d)) + l;
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
@@ -286,7 +289,7 @@ constexpr int kRowNormBlocks = 2048;
 
 template <int LPR, int NV>
 int launch_row_adam(const RowTables& T, const RowList& L, int64_t n_rows, int32_t* last, int32_t* claim,
-                    const int64_t* step, const float2* consts, const AdamK& k, const float* clip, int mode,
+                    const int64_t* step, const float4* consts, const AdamK& k, const float* clip, int mode,
                     hipStream_t s) {
     constexpr int GPB = kBlock / LPR;
     const int64_t n = mode == 2 ? n_rows : L.n_a + L.n_b;
@@ -336,9 +339,10 @@ extern "C" {
 int lgcn_adam_consts(float* consts, int64_t t0, int64_t t1, float lr, double beta1, double beta2,
                      lgcn_stream_t stream) {
     if (!consts || t0 < 1 || t1 < t0) return fail(LGCN_E_ARG, "lgcn_adam_consts: bad range");
+    if (!al16(consts)) return fail(LGCN_E_ARG, "lgcn_adam_consts: consts must be 16-byte aligned");
     const int64_t n = t1 - t0 + 1;
     k_adam_consts<<<grid_for(n, kBlock, int64_t(1) << 30), kBlock, 0, as_stream(stream)>>>(
-        reinterpret_cast<float2*>(consts), t0, t1, lr, beta1, beta2);
+        reinterpret_cast<float4*>(consts), t0, t1, lr, beta1, beta2);
     return check_launch("k_adam_consts");
 }
 
@@ -356,7 +360,8 @@ int lgcn_row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_l
     RowList L{rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b};
     const AdamK k{one_minus_beta1, beta2, one_minus_beta2, eps, beta2 == 0.999f};
     hipStream_t s = as_stream(stream);
-    const auto* c2 = reinterpret_cast<const float2*>(consts);
+    if (!al16(consts)) return fail(LGCN_E_ARG, "lgcn_row_adam: consts must be 16-byte aligned");
+    const auto* c2 = reinterpret_cast<const float4*>(consts);
     int rc = LGCN_OK;
 #define LGCN_RA(LP, NVV) launch_row_adam<LP, NVV>(T, L, n_rows, last, claim, step, c2, k, clip, mode, s)
     auto run = [&]() -> int { LGCN_ROW_DISPATCH(LGCN_RA) };

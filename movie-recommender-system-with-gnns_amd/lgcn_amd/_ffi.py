@@ -25,7 +25,7 @@ E_ARG, E_WORKSPACE, E_UNSUPPORTED = -1, -2, -3  # include/lgcn.h LGCN_E_*
 
 ITEM_BYTES = 16   # lgcn_item_t {int64 beg; int32 len; int32 dst}
 SPLIT_BYTES = 16  # lgcn_split_t {int32 row, pbeg, pcnt, pad}
-ABI_VERSION = 5  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
+ABI_VERSION = 6  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
 
 _lib = None
 

@@ -128,7 +128,8 @@ class RowLazyAdam:
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
         self.steps = 0  # host mirror of the completed steps
         self.max_steps = int(max_steps)
-        self.consts = torch.empty((self.max_steps + 2, 2), dtype=torch.float32, device=dev)
+        # (step size, sqrt(1 - beta2^t), its reciprocal, 0) per step t (lgcn_adam_consts)
+        self.consts = torch.empty((self.max_steps + 2, 4), dtype=torch.float32, device=dev)
         lib = _ffi.load()
         s = _ffi.stream_of(dev)
         _ffi.check(lib.lgcn_adam_consts(self.consts.data_ptr(), 1, self.max_steps + 1, self.lr, float(betas[0]),

@@ -146,7 +146,7 @@ def test_row_adam_padding_never_reads_last(gpu, mode):
     U, I, d = 300, 200, 64
     N = U + I
     s = _ffi.stream_of(gpu)
-    consts = torch.empty((64, 2), device=gpu)
+    consts = torch.empty((64, 4), device=gpu)
     _ffi.check(lib.lgcn_adam_consts(consts.data_ptr(), 1, 62, 1e-3, 0.9, 0.999, s), "consts")
     results = []
     for padded in (False, True):
@@ -190,7 +190,7 @@ def test_adam_consts_are_the_checked_schedule(gpu):
 
     lib = _ffi.load()
     T = 20000
-    consts = torch.zeros((T + 2, 2), device=gpu)
+    consts = torch.zeros((T + 2, 4), device=gpu)
     s = _ffi.stream_of(gpu)
     _ffi.check(lib.lgcn_adam_consts(consts.data_ptr(), 1, T + 1, 1e-3, 0.9, 0.999, s), "consts")
     c = consts.cpu().numpy()
@@ -203,6 +203,8 @@ def test_adam_consts_are_the_checked_schedule(gpu):
     bad = np.nonzero(c[1:, 1].view(np.uint32) != host_c.view(np.uint32))[0]
     assert bad.size == 0, f"device bc2_sqrt differs from host libm at t = {(bad[:8] + 1).tolist()}"
     assert np.array_equal(c[1:, 0].view(np.uint32), host_s.view(np.uint32))
+    # the reciprocal the row Adam multiplies by: fp32 1 / c, correctly rounded (ABI 6)
+    assert np.array_equal(c[1:, 2].view(np.uint32), (np.float32(1.0) / c[1:, 1]).astype(np.float32).view(np.uint32))
     _ffi.check(lib.lgcn_adam_consts(consts.data_ptr(), 1, 10, 1e-3, 0.9, float(np.float32(0.999)), s), "consts")
     assert float(consts[0, 0].item()) == 0.0
 
