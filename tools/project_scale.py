@@ -76,7 +76,7 @@ def main():
     ap.add_argument("--grids", default="8x1,4x2")
     ap.add_argument("--busbw", default="100,150,200,300")
     ap.add_argument("--lat-us", type=float, default=15.0)
-    ap.add_argument("--one-gpu-ms", type=float, default=1.2536, help="the one-GPU K=3 step (BENCH_r03)")
+    ap.add_argument("--one-gpu-ms", type=float, default=1.2205, help="the one-GPU K=3 step (round 4, profiles/r04zd_final)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     g = synth.ml25m_shaped(seed=0)
