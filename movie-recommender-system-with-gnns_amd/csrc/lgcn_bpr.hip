@@ -399,18 +399,27 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
     int64_t base = 0;
     constexpr int64_t kPerRound = int64_t(kRSBlock) * kRSChunks;  // <= kRangeCap: a round always fits an empty list
     static_assert(kPerRound <= kRangeCap, "a round must fit an empty list");
+    // this round's keys (kv) are in registers before the round starts: the next round's are loaded
+    // right after this round's ballots, so their latency overlaps the round's barriers and stores
+    int64_t kv[kRSChunks];
+    auto load_round = [&](int64_t b0, int64_t (&dst)[kRSChunks]) {
+#pragma unroll
+        for (int j = 0; j < kRSChunks; ++j) {
+            const int64_t bj = b0 + (int64_t(wv) * kRSChunks + j) * 64 + lane;
+            dst[j] = bj < B ? keys[bj] : -1;
+        }
+    };
+    load_round(base, kv);
     while (true) {
         // fill the list in b order until full or all keys seen: wave w owns keys
         // [base + w*64*kRSChunks, +64*kRSChunks) of the round, chunk j at + j*64 + lane (coalesced);
         // order inside a wave comes from the ballot masks, across waves from the wave counts
         for (; base < B; base += kPerRound) {
-            int64_t kv[kRSChunks];
             unsigned long long m[kRSChunks];
             int c = 0;
 #pragma unroll
             for (int j = 0; j < kRSChunks; ++j) {
                 const int64_t bj = base + (int64_t(wv) * kRSChunks + j) * 64 + lane;
-                kv[j] = bj < B ? keys[bj] : -1;
                 // keys no workgroup owns (outside [0, nrows)): workgroup 0 clears their flag
                 if (second && blockIdx.x == 0 && bj < B && (kv[j] < 0 || kv[j] >= nrows)) c2flag[bj] = 0;
             }
@@ -419,6 +428,8 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                 m[j] = __ballot(kv[j] >= lo && kv[j] < hi);
                 c += __popcll(m[j]);
             }
+            int64_t kn[kRSChunks];
+            load_round(base + kPerRound, kn);  // the next round's keys, in flight across the barriers
             if (lane == 0) wave_cnt[wv] = c;
             __syncthreads();
             int off = list_n;
@@ -428,7 +439,7 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                 if (w < wv) off += cw;
                 total += cw;
             }
-            if (total > kRangeCap) {  // this round does not fit: flush first, redo it
+            if (total > kRangeCap) {  // this round does not fit: flush first, redo it (kv still holds it)
                 if (threadIdx.x == 0 && overflow) *overflow = 1;  // C2 rows would then be split: report
                 __syncthreads();
                 break;
@@ -445,6 +456,8 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
             __syncthreads();
             if (threadIdx.x == 0) list_n = total;
             __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kRSChunks; ++j) kv[j] = kn[j];
         }
         // sum every row of the list in list order
         const int n = list_n;
