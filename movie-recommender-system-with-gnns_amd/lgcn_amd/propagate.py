@@ -192,6 +192,25 @@ def _forward_sliced_ride(f, N: int, U: int, d: int, x0, acc, K: int, div: float,
                          n_split_big=nb)
 
     pending = None  # the split rows of the last group issued, with their layer's arguments
+    if _launch_timer is not None:
+        # one bracket around all K layers' slice launches (2 events per step; the last combine
+        # launch below stays outside it), so launches x mean <= the step time by construction
+        with _launch_timer(d, K * sum(1 for _, n in f.launches if n)):
+            pending = _ride_layers(f, N, d, K, r, groups, writes, layer, ride_pass, scratch, acc, offs, stream, lib)
+    else:
+        pending = _ride_layers(f, N, d, K, r, groups, writes, layer, ride_pass, scratch, acc, offs, stream, lib)
+    ride = ride_pass(*pending)
+    if ride is not None:
+        _ffi.check(lib.lgcn_spmm_pass(ctypes.byref(ride), N, d, 2, stream), "lgcn_spmm_pass (last combine)")
+
+
+def _ride_layers(f, N, d, K, r, groups, writes, layer, ride_pass, scratch, acc, offs, stream, lib):
+    """The K layers' slice-group launches of _forward_sliced_ride; returns the last group's pending
+    split rows (combined by the caller's final launch)."""
+    import ctypes
+
+    al, ah, as_ = acc
+    pending = None
     for k in range(1, K + 1):
         lay = layer(k)
         xl, xh, xs = lay["x"]
@@ -205,16 +224,9 @@ def _forward_sliced_ride(f, N: int, U: int, d: int, x0, acc, K: int, div: float,
                     _ffi.ptr(lay["y"]), _ffi.ptr(al), _ffi.ptr(ah), as_, _ffi.ptr(lay["part"]), lay["mode"],
                     lay["div"], lay["mul"], stream, run.data_ptr(),
                     ctypes.byref(ride) if ride is not None else None, 0)
-            if _launch_timer is not None:
-                with _launch_timer(d, sum(1 for _, n in f.launches[a:b] if n)):
-                    rc = lib.lgcn_spmm_run_slices_ride(*args)
-            else:
-                rc = lib.lgcn_spmm_run_slices_ride(*args)
-            _ffi.check(rc, "lgcn_spmm_run_slices_ride")
+            _ffi.check(lib.lgcn_spmm_run_slices_ride(*args), "lgcn_spmm_run_slices_ride")
             pending = (writes[grp], lay)
-    ride = ride_pass(*pending)
-    if ride is not None:
-        _ffi.check(lib.lgcn_spmm_pass(ctypes.byref(ride), N, d, 2, stream), "lgcn_spmm_pass (last combine)")
+    return pending
 
 
 def propagate_backward(dout: torch.Tensor, plan: PropagationPlan, U: int, K: int) -> tuple[torch.Tensor, torch.Tensor]:
