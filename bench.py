@@ -279,6 +279,36 @@ def launch_with_fallback(args, launch=None) -> int:
     return rc
 
 
+def parse_tune(items) -> dict:
+    """--tune FIELD=VALUE ... -> {field: value} typed by lgcn_amd.tuning.Tuning (checked here, set by
+    apply_tune in each rank process)."""
+    import dataclasses
+
+    out = {}
+    if not items:
+        return out
+    sys.path.insert(0, str(ROOT / "movie-recommender-system-with-gnns_amd"))
+    from lgcn_amd.tuning import Tuning
+
+    types = {f.name: str(f.type) for f in dataclasses.fields(Tuning)}
+    for it in items:
+        k, _, v = it.partition("=")
+        if k not in types:
+            raise SystemExit(f"--tune: unknown field {k!r} (fields: {', '.join(types)})")
+        t = types[k]
+        out[k] = (v not in ("0", "false", "False") if "bool" in t else
+                  (None if v == "None" else float(v)) if "float" in t else int(v) if "int" in t else v)
+    return out
+
+
+def apply_tune(tuned: dict) -> None:
+    if tuned:
+        from lgcn_amd import tuning
+
+        tuning.set_tuning(**tuned)
+        log(f"tuning: {tuned}")
+
+
 def cpu_share():
     """(CPUs in this process's affinity mask, cgroup CPU quota or None, physical cores of the machine)."""
     aff = len(os.sched_getaffinity(0))
@@ -313,17 +343,25 @@ def cpu_baseline(graph, K, d, seconds_budget=20.0, label="C2"):
     g = torch.Generator().manual_seed(0)
     uw = torch.randn(graph.num_users, d, generator=g) * 0.01
     iw = torch.randn(graph.num_items, d, generator=g) * 0.01
-    runs = {}
-    for threads in counts:  # one cold run per thread count picks the count
+    runs, cold = {}, {}
+    for threads in counts:  # per thread count: a cold run (warm-up), then a warm run picks the count
         torch.set_num_threads(threads)
         t0 = time.perf_counter()
+        cold[threads] = time_reference_forward(uw, iw, ei, K, reps=1, warmup=False)
+        log(f"cpu_baseline: all {ei.shape[1]} edges, {threads} threads, {cold[threads]:.3f} s/forward (cold) "
+            f"({time.perf_counter() - t0:.1f} s total)")
+    best_cold = min(cold.values())
+    for threads in counts:
+        if cold[threads] > 2 * best_cold:  # cannot plausibly win: not worth a warm run
+            runs[threads] = (cold[threads], 1)
+            continue
+        torch.set_num_threads(threads)
         t = time_reference_forward(uw, iw, ei, K, reps=1, warmup=False)
         runs[threads] = (t, 1)
-        log(f"cpu_baseline: all {ei.shape[1]} edges, {threads} threads, {t:.3f} s/forward (cold) "
-            f"({time.perf_counter() - t0:.1f} s total)")
+        log(f"cpu_baseline: {threads} threads, {t:.3f} s/forward (warm)")
     threads = min(runs, key=lambda k: runs[k][0])
     torch.set_num_threads(threads)
-    # the chosen count: its cold run was the warm-up; the median of 3 more
+    # the chosen count: the median of 3 more warm runs
     reps = 3
     t0 = time.perf_counter()
     t = time_reference_forward(uw, iw, ei, K, reps=reps, warmup=False)
@@ -347,7 +385,8 @@ def cpu_baseline(graph, K, d, seconds_budget=20.0, label="C2"):
                                    f"torch.sparse.mm per layer + layer mean, median of 3"},
             "sample": f"all {ei.shape[1]} {label} edges (no sampling), all {graph.num_nodes} nodes, K={K} d={d} forward: "
                       f"index_select -> mul -> scatter_add_ with gcn_norm per layer (PyG 2.4.0 LGConv op sequence, "
-                      f"torch {torch.__version__} CPU), one cold run (warm-up) then the median of {reps}"}
+                      f"torch {torch.__version__} CPU), thread count picked by a warm run after a cold one, then the "
+                      f"median of {reps}"}
 
 
 SETTLE_GROUP = 5        # warm-up steps per settle check
@@ -427,6 +466,9 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="graph scale vs ML-25M (1.0 = C2)")
     ap.add_argument("--chunk", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tune", action="append", default=[], metavar="FIELD=VALUE",
+                    help="A/B: set one lgcn_amd.tuning field for the run (repeatable; the defaults are the "
+                         "measured choices, and the JSON line lists any field set)")
     ap.add_argument("--step-times", action="store_true",
                     help="diagnostic: a HIP event at every timed step boundary; the per-step ms series goes "
                          "into the JSON line (step_ms) and to stderr")
@@ -462,6 +504,7 @@ def main():
                     help="train: reference-style step (compute_embeddings + bpr_loss + autograd) instead of "
                          "the fused no-autograd step")
     args = ap.parse_args()
+    args.tuned = parse_tune(args.tune)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # plain `python bench.py --gpus N`: become the launcher of N ranks (torchrun sets WORLD_SIZE)
         sys.exit(launch_with_fallback(args))
@@ -477,6 +520,7 @@ def main():
     from lgcn_amd.plan import DEFAULT_CHUNK, PropagationPlan, sliced_chunk
     from lgcn_amd.sliced import SlicedDirection
 
+    apply_tune(args.tuned)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -657,7 +701,7 @@ def main():
         settle = settle_warmup(step, torch, dist if distributed else None, dev)
         sliced = isinstance(scheds[0], SlicedDirection)
         # (the ride layout is built by the first forward, so this is known after the warm-up)
-        riding = (sliced and K > 1 and os.environ.get("LGCN_SLICE_RIDE", "1") != "0"
+        riding = (sliced and K > 1 and lgcn_amd.tuning.get().slice_ride
                   and bool(getattr(scheds[0], "_ride", None)))
         # the brackets sample every TIMER_EVERY-th timed step: the riding one-GPU forward brackets a
         # whole step's item-pass launches (2 events; ~0.4 % of a step when every step carries them),
@@ -789,7 +833,9 @@ def main():
         "cpu_baseline": None,
     }
     if sliced:
-        result["config"]["hub_chunk_sliced"] = sliced_chunk(chunk)  # the source-sliced schedule's hub chunk
+        result["config"]["hub_chunk_sliced"] = sliced_chunk(chunk)
+    if args.tuned:
+        result["config"]["tuning"] = args.tuned  # the source-sliced schedule's hub chunk
     if grid_trials is not None:
         result["config"]["grid_trials_ms_per_step"] = grid_trials
     if step_ev is not None:
@@ -826,37 +872,56 @@ def main():
 
 def harness_times(batches, U, I, K, d, dev, epochs=2):
     """ms per step of utils.train_test.train() both ways: the default (the fused batch step,
-    lgcn_amd.harness) and LGCN_HARNESS_FUSED=0 (autograd + torch Adam + clip_grad_norm_); the last
+    lgcn_amd.harness) and tuning harness_fused=False (autograd + torch Adam + clip_grad_norm_); the last
     of `epochs` epochs is timed (the first builds the batch plans and captures the graphs)."""
     import torch
 
     from models.light_gcn import LightGCN
     from utils import train_test as TT
 
+    from lgcn_amd import tuning
+
+    class Fresh:
+        """a loader that collates a new edge_index tensor every iteration (the reference's PyG
+        DataLoader does), on the host (train() moves it) or on the device: the fused step finds
+        each batch's state by content"""
+
+        def __init__(self, where):
+            from data.dataset_handler import Data
+
+            self.Data = Data
+            self.src = [b.edge_index.cpu() for b in batches] if where == "host" else [b.edge_index for b in batches]
+
+        def __len__(self):
+            return len(self.src)
+
+        def __iter__(self):
+            for ei in self.src:
+                yield self.Data(edge_index=ei.clone(), num_nodes=batches[0].num_nodes)
+
     out = {}
-    for name, flag in (("fused_ms_per_step", "1"), ("reference_loop_ms_per_step", "0")):
-        old = os.environ.get("LGCN_HARNESS_FUSED")
-        os.environ["LGCN_HARNESS_FUSED"] = flag
-        try:
+    for name, fused, loader in (("fused_ms_per_step", True, batches),
+                                ("fused_fresh_host_tensors_ms_per_step", True, Fresh("host")),
+                                ("fused_fresh_device_tensors_ms_per_step", True, Fresh("device")),
+                                ("reference_loop_ms_per_step", False, batches)):
+        with tuning.tuned(harness_fused=fused):
             torch.manual_seed(0)
             model = LightGCN(U, I, num_layers=K, dim_h=d).to(dev)
             opt = torch.optim.Adam(model.parameters(), lr=1e-3)
             for e in range(epochs):
                 torch.cuda.synchronize()
                 t = time.perf_counter()
-                TT.train(model, opt, batches, dev)
+                TT.train(model, opt, loader, dev)
                 torch.cuda.synchronize()
                 ms = (time.perf_counter() - t) / len(batches) * 1e3
             out[name] = ms
             out[name.replace("_ms_per_step", "_path")] = TT.LAST_TRAIN_PATH
             del model, opt
-        finally:
-            if old is None:
-                os.environ.pop("LGCN_HARNESS_FUSED", None)
-            else:
-                os.environ["LGCN_HARNESS_FUSED"] = old
     out["note"] = ("utils.train_test.train() per step over one epoch of the bench's batches (the second of two), "
-                   "torch.optim.Adam(lr=1e-3) + clip 1, loss read once per epoch; includes the epoch-end flush")
+                   "torch.optim.Adam(lr=1e-3) + clip 1, loss read once per epoch; includes the epoch-end flush; "
+                   "fused_fresh_*_tensors: the loader yields a new edge_index per batch every epoch, as the "
+                   "reference's PyG DataLoader does (each batch's state found by an XXH3 digest of its bytes; a "
+                   "device tensor is copied to the host for it, one sync per batch)")
     return out
 
 
@@ -878,6 +943,7 @@ def run_train(args):
     from models.light_gcn import LightGCN
     from utils.train_test import bpr_loss, compute_embeddings
 
+    apply_tune(args.tuned)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -1046,6 +1112,8 @@ def run_train(args):
                                     "row-lazy Adam on the union" if exchange is not None else
                                     "RCCL all_reduce of embedding grads" if world > 1 else "single GPU"))},
     }
+    if args.tuned:
+        result["config"]["tuning"] = args.tuned
     if exchange is not None and hasattr(exchange, "bytes"):
         result["exchange"] = {"mode": dp_mode, "MB_received_per_rank_per_step": exchange.bytes / args.steps / 1e6}
     if world == 1 and not args.no_harness:

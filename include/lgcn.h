@@ -38,7 +38,7 @@ extern "C" {
 
 typedef void* lgcn_stream_t; /* a hipStream_t; NULL = the null stream */
 
-#define LGCN_ABI_VERSION 6
+#define LGCN_ABI_VERSION 7
 
 #define LGCN_OK 0
 #define LGCN_E_ARG (-1)         /* bad size / null pointer / unsupported argument */
@@ -89,6 +89,35 @@ int lgcn_abi_version(void);
 /* sha256 (hex) of the sources this library was compiled from: every csrc translation unit,
  * lgcn_common.h and this header (build provenance; lgcn_amd._ffi refuses a mismatch). */
 const char* lgcn_source_sha256(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Tuning (ABI 7). The schedule choices earlier builds read from environment variables at every
+ * dispatch (A/B knobs) are one process-wide struct now; the library reads no environment.
+ * Every default is the measured choice, so a caller that never calls lgcn_set_tuning gets the
+ * tuned library. lgcn_set_tuning validates the whole struct (LGCN_E_ARG on any field out of
+ * range, nothing changed) and replaces it; call it before issuing work, not concurrently with
+ * calls that launch kernels. None of the fields changes a result's bits except where noted
+ * (partition_*: a different, equally valid partition).
+ */
+typedef struct {
+    /* item-pass predicated tail (a row's last < 8 edges per batch gathered together):
+     * -1 = per-launch default (on for d <= 64 and for plain launches of <= 65,536 items), 0 off, 1 on */
+    int32_t spmm_tail;
+    /* index load rounds (batches of col/val per load round): 0 = per-width default, else one of
+     * 1, 2, 4, 8, 16, 32 (widths without that instance keep their default) */
+    int32_t spmm_index_rounds;
+    /* lgcn_spmm_pair: XCDs (of 8) whose workgroup slots run pass a; 0 = a's blocks then b's */
+    int32_t pair_xcds_a;
+    /* host partitioner (lgcn_partition_*): label-propagation refinement rounds, clustering rounds */
+    int32_t partition_refine_rounds;
+    int32_t partition_cluster_rounds;
+    /* lgcn_legacy_choice: host threads replaying the shuffles (1..256) */
+    int32_t choice_threads;
+    int32_t reserved[10]; /* must be zero */
+} lgcn_tuning_t;
+int lgcn_tuning_defaults(lgcn_tuning_t* t);
+int lgcn_set_tuning(const lgcn_tuning_t* t);
+int lgcn_get_tuning(lgcn_tuning_t* t);
 
 /* ---------------------------------------------------------------------------------------
  * CSR construction. Stable counting sort of the edge list by `key`:
@@ -295,9 +324,11 @@ typedef struct {
     float div;
     float mul;
     /* combine layout: -1 = every split row gets a workgroup (lgcn_spmm's combine); n >= 0 = split
-     * rows [0, n) may have any chunk count, rows [n, n_splits) have at most 16 chunks (pcnt <= 16)
-     * and are combined one per lane group instead — the same association, so the same bits, with
-     * a fraction of the workgroups (a rank plan has thousands of 2-16-chunk split rows) */
+     * rows [0, n) get a workgroup each, rows [n, n_splits) are combined one per lane group instead
+     * — the same association, so the same bits, with a fraction of the workgroups (a rank plan has
+     * thousands of 2-16-chunk split rows). Rows of <= 16 chunks (pcnt <= 16) belong after n (as
+     * pack_split_rows orders them); a longer row there is still combined exactly, one running sum
+     * at a time by its lane group, only slower */
     int64_t n_split_big;
 } lgcn_pass_t;
 int lgcn_spmm_pair(const lgcn_pass_t* a, const lgcn_pass_t* b, int64_t N, int32_t d, int32_t what,

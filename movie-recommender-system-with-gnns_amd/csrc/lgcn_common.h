@@ -1,5 +1,6 @@
-// Shared helpers for liblgcn.so (gfx950). Error state is thread-local; no global mutable
-// state otherwise, so every entry point is re-entrant across threads and devices.
+// Shared helpers for liblgcn.so (gfx950). Error state is thread-local; the only other global
+// state is the process-wide tuning struct (lgcn_set_tuning, set before work is issued), so every
+// entry point is re-entrant across threads and devices.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -32,6 +33,9 @@ inline int check_hip(hipError_t e, const char* what) {
 
 // A kernel launch error is reported by hipGetLastError(); it never synchronises.
 inline int check_launch(const char* what) { return check_hip(hipGetLastError(), what); }
+
+// The process-wide tuning (csrc/lgcn_tuning.cpp; defaults = the measured choices).
+const lgcn_tuning_t& tuning();
 
 inline hipStream_t as_stream(lgcn_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -33,28 +33,20 @@
 #include <cstring>
 #include <vector>
 
-#include "lgcn.h"
+#include "lgcn_common.h"
 
 namespace {
 
 thread_local char g_perr[256];
 
-constexpr int kRefineRounds = 16;
 
-// LGCN_PARTITION_REFINE overrides the refinement rounds (A/B tuning; 0 = LDG only)
-int refine_rounds() {
-    const char* v = std::getenv("LGCN_PARTITION_REFINE");
-    return v ? std::atoi(v) : kRefineRounds;
-}
+// lgcn_tuning_t.partition_refine_rounds: the refinement rounds (default 16; 0 = LDG only)
+int refine_rounds() { return lgcn::tuning().partition_refine_rounds; }
 
-constexpr int kClusterRounds = 8;
 
-// LGCN_PARTITION_CLUSTER overrides the clustering rounds of the initial phase (0 = stream the
-// nodes themselves, the round-1 partitioner)
-int cluster_rounds() {
-    const char* v = std::getenv("LGCN_PARTITION_CLUSTER");
-    return v ? std::atoi(v) : kClusterRounds;
-}
+// lgcn_tuning_t.partition_cluster_rounds: the clustering rounds of the initial phase (default
+// 8; 0 = stream the nodes themselves, the round-1 partitioner)
+int cluster_rounds() { return lgcn::tuning().partition_cluster_rounds; }
 
 // Size-constrained label-propagation clustering (KaHIP's SCLaP, used there for coarsening):
 // every node starts alone; in `order`, a node joins the neighbouring cluster holding strictly more

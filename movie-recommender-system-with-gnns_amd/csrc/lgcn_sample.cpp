@@ -178,8 +178,7 @@ void one_choice(MT19937& g, int64_t n, int64_t size, int32_t* xs, int64_t* o) {
 
 int choice_threads(int64_t n, int64_t draws) {
     if (draws < 2 || n < 65536) return 1;
-    int t = 16;
-    if (const char* e = std::getenv("LGCN_CHOICE_THREADS")) t = std::atoi(e);
+    int t = lgcn::tuning().choice_threads;
     const unsigned hw = std::thread::hardware_concurrency();
     if (hw > 0 && static_cast<unsigned>(t) > hw) t = static_cast<int>(hw);
     if (t > draws) t = static_cast<int>(draws);

@@ -418,12 +418,8 @@ __global__ __launch_bounds__(kBlock) void k_spmm_pair(SpmmArgs a, SpmmArgs b, in
 
 // lgcn_spmm_pair's XCDs for pass a: 4 by default (reduce-mode 4 x 2 rank step, K=3, C2: 0.193 ->
 // 0.176 ms against a's blocks then b's; 8 x 1 0.182 vs 0.184, profiles/r04a_pair/);
-// LGCN_PAIR_XCD = 0 (sequential) or 1..7 overrides (A/B).
-int pair_xcd_a() {
-    const char* v = std::getenv("LGCN_PAIR_XCD");
-    const int x = v ? std::atoi(v) : 4;
-    return x < 0 || x > 7 ? 4 : x;
-}
+// lgcn_tuning_t.pair_xcds_a = 0 (sequential) or 1..7 overrides.
+int pair_xcd_a() { return tuning().pair_xcds_a; }
 
 // Split rows: one workgroup per split row. Running sum v (of kVSums, owned by lane group v % GPB)
 // adds partials v, v + kVSums, ... in that order; the kVSums sums are then added in v order through
@@ -497,6 +493,25 @@ __device__ __forceinline__ void combine_small_row(const SpmmArgs& a, int64_t s, 
     const float4* p = reinterpret_cast<const float4*>(a.partial) + int64_t(sp.pbeg) * d4 + l;
     const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = zero;
+    if (sp.pcnt > kVSums) {
+        // outside the packed-row contract (pack_split_rows / ride_layout put only rows of <=
+        // kVSums chunks here): still combine_row's association — running sum v = 0 + p_v +
+        // p_{v+kVSums} + ..., the sums added in v order — one sum at a time (2 x NV registers)
+        for (int v = 0; v < kVSums; ++v) {
+            float4 s[NV];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) s[k] = zero;
+            for (int c = v; c < sp.pcnt; c += kVSums)
+#pragma unroll
+                for (int k = 0; k < NV; ++k) s[k] = f4_add(s[k], p[int64_t(c) * d4 + k * LPR]);
+#pragma unroll
+            for (int k = 0; k < NV; ++k) acc[k] = v == 0 ? s[k] : f4_add(acc[k], s[k]);
+        }
+        finish_row_vec<LPR, NV>(a, sp.row, l, acc);
+        return;
+    }
     for (int c0 = 0; c0 < sp.pcnt; c0 += B) {
         float4 t[B][NV];
 #pragma unroll
@@ -691,11 +706,6 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass, const SpmmArgs* b = n
     return LGCN_OK;
 }
 
-// Kernel-variant override for A/B tuning (LGCN_SPMM_VARIANT; 0 = default choice).
-int spmm_variant() {
-    const char* v = std::getenv("LGCN_SPMM_VARIANT");
-    return v ? std::atoi(v) : 0;
-}
 
 int launch_scalar(const SpmmArgs& a, hipStream_t s, int pass) {
     constexpr int GPB = kBlock / 64;
@@ -712,11 +722,6 @@ int launch_scalar(const SpmmArgs& a, hipStream_t s, int pass) {
     return LGCN_OK;
 }
 
-// Index-load-round override for A/B tuning (LGCN_SPMM_CM; 0 = default choice).
-int spmm_cm() {
-    const char* v = std::getenv("LGCN_SPMM_CM");
-    return v ? std::atoi(v) : 0;
-}
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
@@ -815,8 +820,9 @@ int dispatch(SpmmArgs& a, int64_t N, hipStream_t s, int pass, float* run, const 
     // for sliced launches and for tables beyond the Infinity Cache (C5); off for plain launches
     // over cache-resident tables — the sharded ranks' plain schedule measured +2-3 % with it (their
     // y is the next layer's gathered table) — and for block-split Cluster-GCN launches (+2.6 %).
+    // (Re-checked on the round-4 sliced schedule: 3 / 0 / 1 / 2 -> 1.217 / 1.226 / 1.233 / 1.218 ms,
+    // profiles/r04zk_nt/ — settled, so no longer a knob.)
     a.nt = (pass != PASS_BSPLIT && (run != nullptr || N * int64_t(d) * 4 > (int64_t(512) << 20))) ? 3 : 0;
-    if (const char* nt = std::getenv("LGCN_SPMM_NT")) a.nt = std::atoi(nt);
     SpmmArgs bb;
     if (b != nullptr) {
         bb = *b;
@@ -834,18 +840,20 @@ int dispatch(SpmmArgs& a, int64_t N, hipStream_t s, int pass, float* run, const 
         // d >= 32), so it is on where latency, not loads in flight, bounds the pass: d <= 64, and
         // small plain-schedule launches (Cluster-GCN batch plans). Measured (profiles/r01k_tail/):
         // C2 d=32 -6 %, d=64 -2 %, C3 training step -5 %; C2 d=128 / d=256 +3 % (kept off there).
-        // LGCN_SPMM_VARIANT (A/B knob): 1 = 16-deep unroll at d=64, 2 = tail on, 3 = tail off.
-        const int v = spmm_variant();
-        const bool tail = v == 2 || (v != 1 && v != 3 && (d <= 64 || (run == nullptr && n_items <= 65536)));
+        // lgcn_tuning_t.spmm_tail: -1 = this choice, 0 / 1 = forced off / on. (The 16-deep
+        // unroll at d = 64, once variant 1 of this knob, measured within 1 % or slower in every
+        // round: removed.)
+        const int tv = tuning().spmm_tail;
+        const bool tail = tv == 1 || (tv < 0 && (d <= 64 || (run == nullptr && n_items <= 65536)));
         // Index load rounds (CM batches of LPR edges per col/val load): one or two 128-B lines of
         // col per round at narrow rows, on every launch but the block-split Cluster-GCN batch plans
         // (at d = 128 the C3 step measured +11 % with CM = 4, so d >= 128 keeps one batch per round).
         // Measured (profiles/r02x_cm/): C2 K=3 d=64 1.317 -> 1.269 ms (CM 4), d=32 0.791 -> 0.742
         // (CM 4), d=16 0.859 -> 0.610 (CM 16), d=8 1.354 -> 0.773 (CM 32); d=128/256 slower (kept at 1).
         // The narrow-row round path at d=32 measured the same as per-batch (0.739 vs 0.743 ms), at d=64
-        // +5 %. LGCN_SPMM_CM overrides.
+        // +5 %. lgcn_tuning_t.spmm_index_rounds overrides.
         const bool rounds = pass != PASS_BSPLIT;
-        const int cm = spmm_cm();
+        const int cm = tuning().spmm_index_rounds;
         if (tail) {
             switch (d) {
                 case 4: return (cm ? cm : rounds ? 32 : 8) == 32 ? launch_vec<1, 1, 8, 1, 32>(a, s, pass, b)
@@ -882,7 +890,7 @@ int dispatch(SpmmArgs& a, int64_t N, hipStream_t s, int pass, float* run, const 
             case 8: return launch_vec<2, 1, 8, 0, 4>(a, s, pass, b);
             case 16: return launch_vec<4, 1, 8, 0, 2>(a, s, pass, b);
             case 32: return launch_vec<8, 1, 8>(a, s, pass, b);
-            case 64: return v == 1 ? launch_vec<16, 1, 16>(a, s, pass, b) : launch_vec<16, 1, 8>(a, s, pass, b);
+            case 64: return launch_vec<16, 1, 8>(a, s, pass, b);
             case 128: return launch_vec<32, 1, 8>(a, s, pass, b);
             case 256: return launch_vec<64, 1, 8>(a, s, pass, b);
             case 512: return launch_vec<64, 2, 4>(a, s, pass, b);

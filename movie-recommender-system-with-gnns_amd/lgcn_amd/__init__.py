@@ -4,8 +4,10 @@ Public pieces:
     PropagationPlan / PlanCache   device CSR + gcn_norm weights + load-balanced schedule
     lightgcn_propagate            K-layer propagation with autograd (one node)
     LGConv                        single-layer operator with the PyG LGConv call signature
+    tuning / set_tuning           the process-wide schedule choices (no environment variables)
 """
-from . import _ffi
+from . import _ffi, tuning
+from .tuning import set_tuning
 from .plan import DEFAULT_CHUNK, CsrDirection, PlanCache, PropagationPlan
 from .propagate import (LGConvFunction, LightGCNPropagation, lightgcn_propagate, propagate_backward,
                         propagate_forward, set_launch_timer)
@@ -36,4 +38,5 @@ class LGConv(_torch.nn.Module):
 
 
 __all__ = ["DEFAULT_CHUNK", "CsrDirection", "PlanCache", "PropagationPlan", "LGConv", "LightGCNPropagation",
-           "lightgcn_propagate", "propagate_forward", "propagate_backward", "set_launch_timer", "_ffi"]
+           "lightgcn_propagate", "propagate_forward", "propagate_backward", "set_launch_timer", "set_tuning",
+           "tuning", "_ffi"]

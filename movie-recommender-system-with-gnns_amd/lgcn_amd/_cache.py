@@ -1,0 +1,117 @@
+"""Per-batch caches keyed by the batch's CONTENT, not the tensor object.
+
+The reference's loader (PyG DataLoader(batch_size=1, shuffle=True), reference
+data/dataset_handler.py:285) collates a new Batch, and so a new edge_index tensor, on every
+iteration; keyed by id() every epoch would miss and rebuild what a batch needs (plans, device
+copies, captured hipGraphs) while the dead entries piled up. Here an entry is found by:
+
+  1. the tensor object itself (id + weakref + in-place version counter): no hashing, no sync;
+  2. else its content key: (device, dtype, shape, 128-bit XXH3 digest of its bytes; BLAKE2b
+     where the xxhash module is absent) — a CPU tensor is hashed in place (a C3 batch's 320 KB
+     in ~25 us); a device tensor is copied to the host once (one sync, paid only on an object
+     miss, which otherwise costs a whole plan build).
+
+Entries live in an LRU of bounded size (least recently used evicted first). The id -> key memo
+is shared by every cache (a tensor is hashed at most once while it lives unmodified) and drops the
+entries of freed tensors as it grows.
+"""
+from __future__ import annotations
+
+import collections
+import hashlib
+import weakref
+
+import torch
+
+try:  # ~35x faster than BLAKE2b on a batch's bytes (measured: 25 vs 860 us for 320 KB)
+    import xxhash
+
+    def _digest(buf) -> bytes:
+        return xxhash.xxh3_128(buf).digest()
+except ImportError:  # pragma: no cover - xxhash ships with the image
+    def _digest(buf) -> bytes:
+        return hashlib.blake2b(buf, digest_size=16).digest()
+
+
+def content_key(t: torch.Tensor, extra: tuple = ()) -> tuple:
+    """(device, dtype, shape, digest of the bytes, *extra): equal for tensors of equal content."""
+    host = t.detach()
+    if host.device.type != "cpu":
+        host = host.cpu()
+    host = host.contiguous()
+    digest = _digest(host.numpy().view("uint8").data if host.numel() else b"")
+    return (str(t.device), str(t.dtype), tuple(t.shape), digest, *extra)
+
+
+# id(tensor) -> (weakref, version, content key): shared by every cache, so a tensor is hashed once
+_KEYS: dict[int, tuple[weakref.ref, int, tuple]] = {}
+
+
+def tensor_key(t: torch.Tensor) -> tuple:
+    """content_key(t), memoised on the tensor object while it lives and is not modified in place."""
+    hit = _KEYS.get(id(t))
+    if hit is not None:
+        ref, ver, key = hit
+        if ref() is t and ver == t._version:
+            return key
+    key = content_key(t)
+    _KEYS[id(t)] = (weakref.ref(t), t._version, key)
+    if len(_KEYS) > 64 and len(_KEYS) % 64 == 0:  # amortised: drop the entries of freed tensors
+        for k in [k for k, (r, _, _) in _KEYS.items() if r() is None]:
+            del _KEYS[k]
+    return key
+
+
+def _memo_hit(t: torch.Tensor) -> bool:
+    hit = _KEYS.get(id(t))
+    return hit is not None and hit[0]() is t and hit[1] == t._version
+
+
+class ContentLRU:
+    """value = cache.get(t, build, extra=()): the value built for a tensor of t's content (and the
+    same `extra`), building it with build() on a miss."""
+
+    def __init__(self, capacity: int):
+        if capacity < 1:
+            raise ValueError("capacity must be >= 1")
+        self.capacity = int(capacity)
+        self._values: "collections.OrderedDict[tuple, object]" = collections.OrderedDict()
+        self.hits_object = self.hits_content = self.misses = 0
+
+    @staticmethod
+    def key_of(t: torch.Tensor, extra: tuple = ()) -> tuple:
+        return tensor_key(t) + tuple(extra)
+
+    def __contains__(self, key: tuple) -> bool:
+        return key in self._values
+
+    def get(self, t: torch.Tensor, build, extra: tuple = ()):
+        memo = _memo_hit(t)
+        key = self.key_of(t, extra)
+        if key in self._values:
+            self._values.move_to_end(key)
+            if memo:
+                self.hits_object += 1
+            else:
+                self.hits_content += 1
+            return self._values[key]
+        self.misses += 1
+        value = build()
+        self._values[key] = value
+        while len(self._values) > self.capacity:
+            self._values.popitem(last=False)
+        return value
+
+    def values(self):
+        return list(self._values.values())
+
+    def resize(self, capacity: int) -> None:
+        self.capacity = max(1, int(capacity))
+        while len(self._values) > self.capacity:
+            self._values.popitem(last=False)
+
+    def clear(self) -> None:
+        self._values.clear()
+
+    def __len__(self) -> int:
+        return len(self._values)

@@ -25,7 +25,7 @@ E_ARG, E_WORKSPACE, E_UNSUPPORTED = -1, -2, -3  # include/lgcn.h LGCN_E_*
 
 ITEM_BYTES = 16   # lgcn_item_t {int64 beg; int32 len; int32 dst}
 SPLIT_BYTES = 16  # lgcn_split_t {int32 row, pbeg, pcnt, pad}
-ABI_VERSION = 6  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
+ABI_VERSION = 7  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
 
 _lib = None
 
@@ -41,6 +41,9 @@ _SIGS = {
     "lgcn_last_error": ([], ctypes.c_char_p),
     "lgcn_abi_version": ([], ctypes.c_int),
     "lgcn_source_sha256": ([], ctypes.c_char_p),
+    "lgcn_tuning_defaults": ([_vp], ctypes.c_int),
+    "lgcn_set_tuning": ([_vp], ctypes.c_int),
+    "lgcn_get_tuning": ([_vp], ctypes.c_int),
     "lgcn_csr_workspace_size": ([_i64, _i64, ctypes.POINTER(_sz)], ctypes.c_int),
     "lgcn_csr_build": ([_vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
     "lgcn_group_keys": ([_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
@@ -153,6 +156,14 @@ class Pass(ctypes.Structure):
         self.n_split_big = n_split_big
 
 
+class Tuning(ctypes.Structure):
+    """lgcn_tuning_t (include/lgcn.h, ABI 7)."""
+    _fields_ = [("spmm_tail", ctypes.c_int32), ("spmm_index_rounds", ctypes.c_int32),
+                ("pair_xcds_a", ctypes.c_int32), ("partition_refine_rounds", ctypes.c_int32),
+                ("partition_cluster_rounds", ctypes.c_int32), ("choice_threads", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 10)]
+
+
 class LgcnError(RuntimeError):
     pass
 
@@ -186,7 +197,7 @@ CSRC = _HERE.parent / "csrc"
 INCLUDE = _HERE.parent.parent / "include"
 # the translation units of liblgcn.so (lgcn_build.cpp carries the hash and is not hashed)
 SOURCES = ("lgcn_plan.hip", "lgcn_spmm.hip", "lgcn_optim.hip", "lgcn_bpr.hip", "lgcn_recall.hip", "lgcn_rowadam.hip",
-           "lgcn_exchange.hip", "lgcn_partition.cpp", "lgcn_sample.cpp")
+           "lgcn_exchange.hip", "lgcn_partition.cpp", "lgcn_sample.cpp", "lgcn_tuning.cpp")
 
 
 def source_sha256() -> str:

@@ -16,7 +16,6 @@ the union of the ranks' rows.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.distributed as dist
@@ -25,10 +24,13 @@ import torch.distributed as dist
 def device_collectives(group=None) -> bool:
     """True where the multi-GPU paths run their collectives on device tensors in stream order
     (backend "nccl" = RCCL): side streams, events, in-place views, no host staging. gloo runs the
-    same calls on CUDA tensors too (tools/rccl_probe.py --backend gloo), so LGCN_DEVICE_COLLECTIVES=1
-    sends a gloo run down that branch — how the ranks-on-one-GPU tests exercise the code the RCCL
-    runs take, since RCCL refuses two ranks on one GPU."""
-    if os.environ.get("LGCN_DEVICE_COLLECTIVES") == "1":
+    same calls on CUDA tensors too (tools/rccl_probe.py --backend gloo), so
+    lgcn_amd.tuning's device_collectives=True sends a gloo run down that branch — how the
+    ranks-on-one-GPU tests exercise the code the RCCL runs take, since RCCL refuses two ranks on
+    one GPU."""
+    from . import tuning
+
+    if tuning.get().device_collectives:
         return True
     return dist.get_backend(group) == "nccl"
 

@@ -13,7 +13,7 @@ torch.optim.Adam over exactly its two tables (one param group, betas (0.9, 0.999
 weight decay / amsgrad / maximize / capturable / differentiable), d in {16, ..., 512}, and batches
 that are bipartite user-item edge lists (the reference's triplets pair the k-th user-source edge's
 user with its item).
-LGCN_HARNESS_FUSED=0 forces the reference-style step.
+lgcn_amd.tuning.set_tuning(harness_fused=False) forces the reference-style step.
 
 What the caller sees is what the reference loop leaves: the model's tables and the torch
 optimizer's state (exp_avg, exp_avg_sq, step per table) after the epoch — the row-lazy Adam is
@@ -26,24 +26,24 @@ optimizer's own tables, not .grad; the reference leaves the last batch's gradien
 """
 from __future__ import annotations
 
-import os
 import weakref
 
 import torch
 
-from . import _ffi
 
 _DIMS = (16, 32, 64, 128, 256, 512)
 
 
 def enabled() -> bool:
-    return os.environ.get("LGCN_HARNESS_FUSED", "1") != "0"
+    from . import tuning
+
+    return tuning.get().harness_fused
 
 
 def eligibility(model, optimizer) -> str | None:
     """None when train(model, optimizer, ...) can run on the fused step, else the reason not."""
     if not enabled():
-        return "LGCN_HARNESS_FUSED=0"
+        return "tuning harness_fused=False"
     for a in ("num_users", "num_items", "num_layers", "dim_h", "user_embedding", "item_embedding"):
         if not hasattr(model, a):
             return f"model has no {a} (not a LightGCN)"
@@ -72,10 +72,17 @@ def eligibility(model, optimizer) -> str | None:
     return None
 
 
+# batch states kept per (model, optimizer) beyond one epoch's batches (lgcn_amd._cache LRU)
+_MIN_STATES = 64
+# first size of the row-lazy Adam's per-step constant table (16 B per step; grown by doubling)
+_MIN_STEPS = 4096
+
+
 class _Fast:
     """The fused step and row-lazy Adam attached to one (model, torch optimizer) pair."""
 
     def __init__(self, model, optimizer):
+        from ._cache import ContentLRU
         from .optim import RowLazyAdam
         from .train_step import FusedTrainStep
 
@@ -83,41 +90,52 @@ class _Fast:
         self.model = model
         self.lr = float(g["lr"])
         uw, iw = model.user_embedding.weight, model.item_embedding.weight
-        self.opt = RowLazyAdam(uw.data, iw.data, lr=self.lr, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=1.0)
+        self.opt = RowLazyAdam(uw.data, iw.data, lr=self.lr, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=1.0,
+                               max_steps=_MIN_STEPS)
         from utils import helpers
 
         num_items, dev = model.num_items, uw.device
         # the negatives come from the harness's own sampler (reference utils/helpers.py:64-82):
         # the reference loop's draws, and whatever a caller substitutes for them
-        self.step = FusedTrainStep(model, self.opt, lazy=True, graphs=True,
+        self.step = FusedTrainStep(model, self.opt, lazy=True, graphs=True, max_entries=_MIN_STATES,
                                    neg_sampler=lambda pos: helpers.sample_negative(pos, num_items, dev))
-        # device copies of the loader's batches (keyed by the host edge_index, held weakly), so a
-        # batch keeps its plans and captured graph from epoch to epoch
-        self.dev_batches: dict[int, tuple[weakref.ref, torch.Tensor]] = {}
+        # device copies of host batches by content, so a batch keeps its plans and captured graph
+        # from epoch to epoch even when the loader collates a new tensor each time
+        self.dev_batches = ContentLRU(_MIN_STATES)
+        # batch contents already checked bipartite (an object / content hit skips the check)
+        self.checked = ContentLRU(_MIN_STATES)
+
+    def size_for(self, n_batches: int | None) -> None:
+        """Caches for one epoch of n_batches (plus slack), constants for this epoch's steps; called
+        at an epoch's start, when every row is current."""
+        if n_batches:
+            cap = max(_MIN_STATES, 2 * n_batches)
+            for c in (self.step._states, self.dev_batches, self.checked):
+                c.resize(cap)
+            self.reserve(self.opt.steps + n_batches)
+
+    def reserve(self, steps: int) -> None:
+        if self.opt.reserve(steps):
+            self.step.drop_graphs()  # the captured steps read the old constant table
 
     def device_edge_index(self, ei: torch.Tensor, device) -> torch.Tensor:
         if ei.is_cuda:
             return ei
-        hit = self.dev_batches.get(id(ei))
-        if hit is not None and hit[0]() is ei and hit[1].shape == ei.shape:
-            return hit[1]
-        d = ei.to(device)
-        self.dev_batches[id(ei)] = (weakref.ref(ei), d)
-        if len(self.dev_batches) > 4096:
-            for k in [k for k, (r, _) in self.dev_batches.items() if r() is None]:
-                self.dev_batches.pop(k)
-        return d
+        return self.dev_batches.get(ei, lambda: ei.to(device))
+
+    def eligible(self, ei: torch.Tensor, U: int) -> bool:
+        """The batch is a bipartite user-item edge list (checked once per content)."""
+        return bool(self.checked.get(ei, lambda: bipartite(ei, U)))
 
     # --- torch optimizer state <-> row-lazy Adam -----------------------------------------------
     def load_state(self, optimizer) -> None:
         """Start from the torch optimizer's state (none yet: step 0, zero moments)."""
         g = optimizer.param_groups[0]
         if float(g["lr"]) != self.lr:  # an lr change between epochs: new step constants
+            # (every row is current here, so no past step is replayed with them)
             self.lr = float(g["lr"])
             self.opt.lr = self.lr
-            lib = _ffi.load()
-            _ffi.check(lib.lgcn_adam_consts(self.opt.consts.data_ptr(), 1, self.opt.max_steps + 1, self.lr, 0.9,
-                                            0.999, _ffi.stream_of(self.opt.device)), "lgcn_adam_consts")
+            self.opt.regenerate_consts()
         uw, iw = self.model.user_embedding.weight, self.model.item_embedding.weight
         steps = None
         for i, p in enumerate((uw, iw)):
@@ -161,46 +179,44 @@ def bipartite(ei: torch.Tensor, U: int) -> bool:
     return bool(((ei[0] < U) == (ei[1] >= U)).all().item())
 
 
-def train_epoch(model, optimizer, train_loader, device) -> tuple[float, int] | None:
-    """One train() epoch on the fused step: (sum over batches of loss * edges, total edges), or None
-    if a batch is not eligible before any step ran (the caller then runs the reference loop)."""
+def train_epoch(model, optimizer, batches, device):
+    """Run the fused step over the batches iterator until it ends or yields a batch the fused step
+    cannot take (not a bipartite user-item edge list). Returns (sum over the fused batches of
+    loss * edges as a device tensor or None, their total edges, the first batch not taken or None,
+    fused steps run). The torch optimizer holds the row-lazy Adam's state whenever this returns,
+    so the caller runs the reference loop from the returned batch on (the iterator is read once:
+    one-shot loaders lose no batch)."""
     fast = _FAST.get(optimizer)
     if fast is None or fast.model is not model:
         fast = _Fast(model, optimizer)
         _FAST[optimizer] = fast
-    fast.load_state(optimizer)
-    total, total_w = None, 0
-    U = model.num_users
-    bad = object()  # a batch the fused step cannot take
-
-    def device_batches():
-        for batch in train_loader:
-            ei = fast.device_edge_index(batch.edge_index, device)
-            st = fast.step._states.get(id(ei))
-            yield bad if (st is None or st[0]() is not ei) and not bipartite(ei, U) else ei
-
     try:
-        it = device_batches()
-        ei = next(it, None)
-        if ei is bad:
-            return None  # nothing ran: the caller runs the reference loop
-        while ei is not None:
-            nxt = next(it, None)
-            if nxt is bad:
-                raise ValueError("train(): a batch is not a bipartite user-item edge list; run with "
-                                 "LGCN_HARNESS_FUSED=0")
+        n = len(batches)
+    except TypeError:
+        n = None
+    fast.load_state(optimizer)
+    fast.size_for(n)
+    total, total_w, steps, leftover = None, 0, 0, None
+    U = model.num_users
+    try:
+        for batch in batches:
+            ei = fast.device_edge_index(batch.edge_index, device)
+            if not fast.eligible(ei, U):
+                leftover = batch
+                break
+            if fast.opt.steps + 1 > fast.opt.max_steps:  # a loader without len(): grow mid-epoch
+                fast.step.sync()  # every row current before the constants are regenerated
+                fast.reserve(fast.opt.steps + 1)
             loss = fast.step.step(_Batch(ei))
+            steps += 1
             w = int(ei.shape[1])
             total_w += w
             contrib = loss.detach().double() * w
             total = contrib if total is None else total + contrib
-            ei = nxt
     finally:
-        if total is not None:
+        if steps:
             fast.store_state(optimizer)
-    if total is None:
-        raise ZeroDivisionError("empty train loader")
-    return total.item(), total_w
+    return total, total_w, leftover, steps
 
 
 class _Batch:

@@ -131,14 +131,30 @@ class RowLazyAdam:
         # (step size, sqrt(1 - beta2^t), its reciprocal, 0) per step t (lgcn_adam_consts)
         self.consts = torch.empty((self.max_steps + 2, 4), dtype=torch.float32, device=dev)
         lib = _ffi.load()
-        s = _ffi.stream_of(dev)
-        _ffi.check(lib.lgcn_adam_consts(self.consts.data_ptr(), 1, self.max_steps + 1, self.lr, float(betas[0]),
-                                        float(betas[1]), s), "lgcn_adam_consts")
+        self.regenerate_consts()
         self.norm_ws = torch.empty(lib.lgcn_row_grad_norm_workspace_floats(), dtype=torch.float32, device=dev)
         self.last_norm = torch.zeros(2, dtype=torch.float32, device=dev)
         # gradient tables: rows outside a step's touched set are never written or read
         self.gu = torch.empty_like(user_w)
         self.gi = torch.empty_like(item_w)
+
+    def reserve(self, steps: int) -> bool:
+        """Make room for step constants up to `steps` (at least doubling); True if the constant
+        table moved (hipGraphs captured over the old one must be recaptured). The new table is
+        regenerated whole, from the current lr: call it only when every row is current (load /
+        flush), or the replays of past steps would use the new constants."""
+        if steps <= self.max_steps:
+            return False
+        self.max_steps = max(int(steps), 2 * self.max_steps)
+        self.consts = torch.empty((self.max_steps + 2, 4), dtype=torch.float32, device=self.device)
+        self.regenerate_consts()
+        return True
+
+    def regenerate_consts(self) -> None:
+        """The per-step constants [1, max_steps + 1) from the current lr and betas."""
+        lib = _ffi.load()
+        _ffi.check(lib.lgcn_adam_consts(self.consts.data_ptr(), 1, self.max_steps + 1, self.lr, float(self.betas[0]),
+                                        float(self.betas[1]), _ffi.stream_of(self.device)), "lgcn_adam_consts")
 
     def _tables(self, with_grad: bool):
         p = (self.uw.data_ptr(), self.iw.data_ptr())

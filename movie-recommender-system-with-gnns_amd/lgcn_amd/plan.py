@@ -15,8 +15,6 @@ edge order inside a row, which is the order CPU scatter_add_/index_add_ add in.
 from __future__ import annotations
 
 import dataclasses
-import os
-import weakref
 
 import torch
 
@@ -31,14 +29,13 @@ DEFAULT_CHUNK = 256
 SLICED_CHUNK = 192
 # hub chunk of the plain schedule the sharded forward's ranks run when R > 1 (lgcn_amd.sharded.
 # rank_chunk): per-rank K=3 step at 8 x 1 0.246 ms at 128, 0.253 at 256 (profiles/r02k_shard/)
-RANK_CHUNK = int(os.environ.get("LGCN_RANK_CHUNK", 128))  # (env: A/B knob)
+RANK_CHUNK = 128
 
 
 def sliced_chunk(chunk: int) -> int:
     return min(int(chunk), SLICED_CHUNK)
-# batch plans (touched-only, segment) use the one-launch block-split schedule; LGCN_BLOCKSPLIT=0
-# keeps them on item pass + combine (A/B knob)
-BLOCK_SPLIT = os.environ.get("LGCN_BLOCKSPLIT", "1") != "0"
+# batch plans (touched-only, segment) use the one-launch block-split schedule (C3 step 0.222 ->
+# 0.203 ms, profiles/r01l_blocksplit/) ...
 # ... while no split row has more chunks than this: lgcn_spmm_blocksplit sums a split row in one
 # workgroup (16 running sums, csrc/lgcn_spmm.hip kVSums), so a row of c chunks is a chain of
 # ceil(c / 16) chunks — the launch's critical path. Past 2 chunks per running sum (a structured
@@ -48,8 +45,6 @@ BLOCK_SPLIT_MAX_CHUNKS = 32
 
 
 def _block_split_for(splits: torch.Tensor, n_splits: int) -> bool:
-    if not BLOCK_SPLIT:
-        return False
     return n_splits == 0 or int(splits[:n_splits, 2].max().item()) <= BLOCK_SPLIT_MAX_CHUNKS
 
 
@@ -59,10 +54,12 @@ def slice_bytes_for(num_nodes: int, d: int) -> int:
     table is small enough that re-reading the running row sums once per slice costs less than the
     cache misses it saves — about 8 slices of 8–24 MB for tables of 16–512 MB; beyond that (C5:
     11 GB) the plain schedule is faster. PropagationPlan.schedule also requires >= 8 edges per
-    row per slice. LGCN_SLICE_MB overrides the size and that density test (0 disables)."""
-    env = os.environ.get("LGCN_SLICE_MB")
-    if env is not None:
-        v = float(env)
+    row per slice. lgcn_amd.tuning's slice_mb overrides the size and that density test (0
+    disables)."""
+    from . import tuning
+
+    v = tuning.get().slice_mb
+    if v is not None:
         return int(v * 2**20) if v > 0 else 0
     x = int(num_nodes) * int(d) * 4
     if x < 16 * 2**20 or x > 512 * 2**20:
@@ -283,7 +280,9 @@ class PropagationPlan:
             bounds = slice_bounds(self.num_nodes, self.side_split, d, sb)
             # the running sums cost ~2 row passes per slice: worth it only for dense enough graphs
             # (C2: 112 edges per row; a 5 % validation edge set, ~6, is faster unsliced)
-            forced = os.environ.get("LGCN_SLICE_MB") is not None
+            from . import tuning
+
+            forced = tuning.get().slice_mb is not None
             if forced or self.num_edges >= 8 * (len(bounds) - 1) * self.num_nodes:
                 out = build_sliced(direction, self.num_nodes, bounds, sliced_chunk(direction.chunk)) or direction
         self._sched[key] = out
@@ -310,37 +309,21 @@ class PropagationPlan:
 
 
 class PlanCache:
-    """Plans keyed by the edge_index tensor object (weakly referenced) and its version counter:
-    a tensor that is modified in place or freed never hits a stale plan."""
+    """Plans keyed by the edge_index's content (lgcn_amd._cache: the tensor object itself while it
+    lives unmodified, else a digest of its bytes) plus (num_nodes, side_split): a tensor modified in
+    place never hits a stale plan, and a loader that collates a new tensor of the same edges each
+    epoch reuses its plan. Least recently used plans are evicted beyond max_entries."""
 
-    def __init__(self, max_entries: int = 4096, chunk: int = DEFAULT_CHUNK):
+    def __init__(self, max_entries: int = 1024, chunk: int = DEFAULT_CHUNK):
+        from ._cache import ContentLRU
+
         self.max_entries = max_entries
         self.chunk = chunk
-        self._entries: dict[tuple, tuple[weakref.ref, PropagationPlan]] = {}
+        self._entries = ContentLRU(max_entries)
 
     def get(self, edge_index: torch.Tensor, num_nodes: int, side_split: int = 0) -> PropagationPlan:
-        key = (id(edge_index), edge_index.data_ptr(), tuple(edge_index.shape), tuple(edge_index.stride()),
-               edge_index._version, int(num_nodes), int(side_split), str(edge_index.device))
-        hit = self._entries.get(key)
-        if hit is not None:
-            ref, plan = hit
-            if ref() is edge_index:
-                # LRU refresh
-                self._entries.pop(key)
-                self._entries[key] = hit
-                return plan
-            self._entries.pop(key)
-        plan = PropagationPlan(edge_index, num_nodes, self.chunk, side_split)
-        self._entries[key] = (weakref.ref(edge_index), plan)
-        self._evict()
-        return plan
-
-    def _evict(self) -> None:
-        dead = [k for k, (r, _) in self._entries.items() if r() is None]
-        for k in dead:
-            self._entries.pop(k)
-        while len(self._entries) > self.max_entries:
-            self._entries.pop(next(iter(self._entries)))
+        return self._entries.get(edge_index, lambda: PropagationPlan(edge_index, num_nodes, self.chunk, side_split),
+                                 extra=(int(num_nodes), int(side_split)))
 
     def clear(self) -> None:
         self._entries.clear()

@@ -11,12 +11,11 @@ No intermediate x_k is saved: Â is linear, so the backward needs only the plan 
 """
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import torch
 
-from . import _ffi
+from . import _ffi, tuning
 from .plan import CsrDirection, PropagationPlan
 from .sliced import SlicedDirection, spmm_sliced, spmm_sliced_combine
 
@@ -123,7 +122,7 @@ def propagate_forward(user_w: torch.Tensor, item_w: torch.Tensor, plan: Propagat
                    "lgcn_copy_scale")
         return out
     f = plan.schedule("fwd", d)
-    if (K > 1 and isinstance(f, SlicedDirection) and os.environ.get("LGCN_SLICE_RIDE", "1") != "0"
+    if (K > 1 and isinstance(f, SlicedDirection) and tuning.get().slice_ride
             and d % 4 == 0 and d <= 1024 and (d & (d - 1)) == 0):
         from .sliced import ride_layout
 

@@ -20,12 +20,10 @@ import torch
 
 from . import _ffi
 
-import os
-
-# candidates scored for the first thresholds (≈ k·M/SUBSET survive the filter) and the per-query
-# list capacity (>= SUBSET: the first pass stores every subset score)
-SUBSET = int(os.environ.get("LGCN_RECALL_SUBSET", 16384))
-CAP = max(SUBSET, 16384)
+# candidates scored for the first thresholds (≈ k·M/subset survive the filter; lgcn_amd.tuning's
+# recall_subset, default 16384) and the per-query list capacity (>= the subset: the first pass
+# stores every subset score)
+CAP_MIN = 16384
 
 
 class _Workspace:
@@ -57,9 +55,13 @@ def _normalize_into(lib, x: torch.Tensor, idx, rows: int, out_ptr: int, D: int, 
 
 
 def topk_hits(users: torch.Tensor, picked: torch.Tensor, pos: torch.Tensor, neg: torch.Tensor, k: int,
-              cap: int = CAP, subset: int = SUBSET) -> torch.Tensor:
+              cap: int | None = None, subset: int | None = None) -> torch.Tensor:
     """hits[q] = number of positives (rows of ``pos``) among the top-k cosine scores of
     users[picked[q]] against cat(pos, neg); int32 [Q] on the device."""
+    from . import tuning
+
+    subset = tuning.get().recall_subset if subset is None else int(subset)
+    cap = max(subset, CAP_MIN) if cap is None else int(cap)
     lib = _ffi.load()
     dev = users.device
     for t in (users, pos, neg):

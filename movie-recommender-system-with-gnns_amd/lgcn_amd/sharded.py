@@ -342,9 +342,9 @@ class ShardedPlan:
 
 
 def _slice_forced() -> bool:
-    import os
+    from . import tuning
 
-    return os.environ.get("LGCN_SLICE_MB") is not None
+    return tuning.get().slice_mb is not None
 
 
 EXCHANGE_MODES = ("allgather", "p2p")

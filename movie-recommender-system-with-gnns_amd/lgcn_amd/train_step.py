@@ -24,7 +24,6 @@ negatives are drawn each step. No host synchronisation happens inside a step.
 """
 from __future__ import annotations
 
-import weakref
 
 import torch
 
@@ -226,22 +225,19 @@ class _BatchState:
 
 def neg_grouping() -> str:
     """How the sorted negatives path groups the B keys by row: "count" (lgcn_group_keys, the
-    default) or "radix" (lgcn_csr_build); LGCN_NEG_GROUPING overrides."""
-    import os
+    default) or "radix" (lgcn_csr_build); lgcn_amd.tuning's neg_grouping."""
+    from . import tuning
 
-    g = os.environ.get("LGCN_NEG_GROUPING", "count")
-    if g not in ("count", "radix"):
-        raise ValueError(f"LGCN_NEG_GROUPING={g!r}: expected 'count' or 'radix'")
-    return g
+    return tuning.get().neg_grouping
 
 
 def sorted_scatter_min_b() -> int:
     """Batch size from which the negatives go through the sorted scatter instead of the range
     scatter (whose key streaming grows as B^2): measured on the C3 graphs (B ~ 1e4: range
-    scatter ~10 us; B ~ 1.6e5: 627 us range vs sort + scatter). LGCN_SORTED_SCATTER_MIN_B overrides."""
-    import os
+    scatter ~10 us; B ~ 1.6e5: 627 us range vs sort + scatter). lgcn_amd.tuning's sorted_scatter_min_b."""
+    from . import tuning
 
-    return int(os.environ.get("LGCN_SORTED_SCATTER_MIN_B", 49152))
+    return tuning.get().sorted_scatter_min_b
 
 
 def loss_fused(st, I: int, cols=None) -> bool:
@@ -314,7 +310,7 @@ class FusedTrainStep:
     step(batch) -> device loss tensor [1]: gradients, optional DP all-reduce, optimizer step.
     compute_grads(batch) -> loss: sets user/item_embedding.weight.grad only."""
 
-    def __init__(self, model, optimizer, bpr_coeff: float = 5e-3, world: int = 1, max_entries: int = 4096,
+    def __init__(self, model, optimizer, bpr_coeff: float = 5e-3, world: int = 1, max_entries: int = 1024,
                  graphs: bool = False, lazy: bool = False, exchange=None, neg_seed: int | None = None,
                  cols: ColumnGroup | None = None, neg_sampler=None):
         """graphs=True: the first step of each batch runs eagerly, then the whole step (gradients
@@ -350,7 +346,11 @@ class FusedTrainStep:
                 raise ValueError("lazy=True with world > 1 needs a lgcn_amd.distributed.RowExchange")
         elif graphs and world == 1 and not getattr(optimizer, "capturable", False):
             raise ValueError("graphs=True needs a capturable optimizer (lgcn_amd.optim.FusedAdam(capturable=True))")
-        self._states: dict[int, tuple[weakref.ref, int, _BatchState]] = {}
+        # per-batch states (plans, buffers, captured graphs) by batch content: a loader that
+        # collates a new edge_index each epoch (the reference's PyG DataLoader) still replays
+        from ._cache import ContentLRU
+
+        self._states = ContentLRU(max_entries)
         from .owner import OwnerExchange
 
         self.cols = cols
@@ -370,17 +370,23 @@ class FusedTrainStep:
         self._synced = True  # every row current on every rank (start, or after sync())
 
     def state(self, edge_index: torch.Tensor) -> _BatchState:
-        hit = self._states.get(id(edge_index))
-        if hit is not None:
-            ref, ver, st = hit
-            if ref() is edge_index and ver == edge_index._version:
-                return st
-        st = _BatchState(self.model, edge_index, self.model.dim_h, lazy=self.lazy)
-        self._states[id(edge_index)] = (weakref.ref(edge_index), edge_index._version, st)
-        if len(self._states) > self.max_entries:
-            for k in [k for k, (r, _, _) in self._states.items() if r() is None]:
-                self._states.pop(k)
-        return st
+        """The batch's state, built on the first step of a batch of this content (lgcn_amd._cache:
+        the same tensor object without hashing, else by content; least recently used evicted
+        beyond max_entries)."""
+        return self._states.get(edge_index, lambda: _BatchState(self.model, edge_index, self.model.dim_h,
+                                                                 lazy=self.lazy))
+
+    def drop_graphs(self) -> None:
+        """Forget every batch's captured hipGraph (the next step of each batch recaptures it):
+        needed when a buffer a graph reads moved, e.g. RowLazyAdam.reserve() grew its constants."""
+        for st in self._states.values():
+            for a in ("graph", "graph_post", "graph_loss", "graph_grads"):
+                if hasattr(st, a):
+                    setattr(st, a, None)
+
+    def has_state(self, edge_index: torch.Tensor) -> bool:
+        """A state for a batch of this content exists (its checks already passed)."""
+        return self._states.key_of(edge_index) in self._states
 
     def _draw(self, st, k: int | None = None) -> None:
         """Step k's negatives (reference utils/helpers.py:64-82: torch.randint(0, I, (B,))).
@@ -699,7 +705,7 @@ class FusedTrainStep:
         call once per epoch)."""
         if self.owner:
             self.exchange.check_overflow()
-        for ref, _, st in self._states.values():
+        for st in self._states.values():
             if getattr(st, "overflow", None) is not None and int(st.overflow.item()):
                 raise RuntimeError("lgcn_range_scatter_add overflowed: negatives too concentrated for its lists")
             if getattr(st, "neg_err", None) is not None and int(st.neg_err.item()):

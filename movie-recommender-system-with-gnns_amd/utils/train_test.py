@@ -71,43 +71,76 @@ def compute_embeddings(model: torch.nn.Module, data, device) -> Tuple[torch.Tens
 LAST_TRAIN_PATH = None
 
 
+def _reference_step(model, optimizer, batch, device):
+    """One step of the reference loop (:86-101): (loss * edges as a device tensor, edges)."""
+    batch = batch.to(device)
+    optimizer.zero_grad()
+    loss = bpr_loss(*compute_embeddings(model, batch, device))
+    loss.backward()
+    if getattr(optimizer, "fused_clip_norm", None) is None:
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1)
+    optimizer.step()  # lgcn_amd.optim.FusedAdam(max_grad_norm=1) clips inside its step
+    w = batch.edge_index.shape[1]
+    return loss.detach().double() * w, w
+
+
 def train(model: torch.nn.Module, optimizer: torch.optim.Optimizer, train_loader, device) -> float:
     """One epoch over the loader; returns the edge-weighted mean batch loss (reference :66-103).
     A HIP LightGCN with the reference's torch Adam runs the fused batch step (lgcn_amd.harness:
     HIP forward / BPR / backward and the exact row-lazy Adam, one hipGraph per batch) with the
-    same negatives, loss and optimizer state; anything else runs the reference-style loop below."""
+    same negatives, loss and optimizer state; anything else runs the reference-style loop below —
+    from the first batch the fused step cannot take to the epoch's end (the loader is iterated
+    once, so a one-shot iterator loses no batch)."""
     global LAST_TRAIN_PATH
     model.train()
     why = "model not on a ROCm device"
+    total_loss, total_w = None, 0
+    batches = train_loader
+    rest = None  # the first batch the reference loop takes after fused steps
     weight = getattr(getattr(model, "user_embedding", None), "weight", None)
     if weight is not None and weight.is_cuda:
         from lgcn_amd import harness
 
         why = harness.eligibility(model, optimizer)
         if why is None:
-            res = harness.train_epoch(model, optimizer, train_loader, device)
-            if res is not None:
+            batches = iter(train_loader)
+            if hasattr(train_loader, "__len__"):
+                batches = _Sized(batches, len(train_loader))
+            total_loss, total_w, rest, steps = harness.train_epoch(model, optimizer, batches, device)
+            if rest is None:
                 LAST_TRAIN_PATH = "fused"
-                return res[0] / res[1]
+                if total_loss is None:
+                    raise ZeroDivisionError("empty train loader")
+                return total_loss.item() / total_w
             why = "a batch is not a bipartite user-item edge list"
+            if steps:
+                why = f"fused for {steps} batch(es), then reference from a batch that is not a bipartite user-item edge list"
     LAST_TRAIN_PATH = f"reference: {why}"
-    total_loss = None
-    total_w = 0
-    for batch in train_loader:
-        batch = batch.to(device)
-        optimizer.zero_grad()
-        loss = bpr_loss(*compute_embeddings(model, batch, device))
-        loss.backward()
-        if getattr(optimizer, "fused_clip_norm", None) is None:
-            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1)
-        optimizer.step()  # lgcn_amd.optim.FusedAdam(max_grad_norm=1) clips inside its step
-        w = batch.edge_index.shape[1]
+    for batch in (_chain(rest, batches) if rest is not None else batches):
+        contrib, w = _reference_step(model, optimizer, batch, device)
         total_w += w
-        contrib = loss.detach().double() * w
         total_loss = contrib if total_loss is None else total_loss + contrib
     if total_loss is None:
         raise ZeroDivisionError("empty train loader")
     return total_loss.item() / total_w
+
+
+class _Sized:
+    """An iterator that still reports the loader's len() (the harness sizes its caches by it)."""
+
+    def __init__(self, it, n):
+        self.it, self.n = it, n
+
+    def __iter__(self):
+        return self.it
+
+    def __len__(self):
+        return self.n
+
+
+def _chain(first, rest):
+    yield first
+    yield from rest
 
 
 def compute_recall_at_k(embs, k: int = 20, num_samples: int = 10, sample_size: int = 100, picks=None) -> float:

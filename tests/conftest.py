@@ -18,6 +18,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: full-size parity (minutes on the CPU oracle side)")
 
 
+@pytest.fixture
+def tune():
+    """tune(field=value, ...): lgcn_amd.tuning.set_tuning for one test, the previous record restored
+    after it (the path reads no environment variables)."""
+    import dataclasses
+
+    from lgcn_amd import tuning
+
+    saved = tuning.get()
+    yield tuning.set_tuning
+    tuning.set_tuning(**dataclasses.asdict(saved))
+
+
 @pytest.fixture(scope="session")
 def gpu():
     import torch

@@ -36,7 +36,10 @@ def main():
 
     import graphs
     from lgcn_amd import cluster as C
-    from lgcn_amd import _ffi
+    from lgcn_amd import _ffi, tuning
+
+    if os.environ.get("DP_DEVICE_COLLECTIVES") == "1":  # the RCCL branches, gloo carrying the bytes
+        tuning.set_tuning(device_collectives=True)
     from lgcn_amd import distributed as D
     from lgcn_amd.optim import FusedAdam, RowLazyAdam
     from lgcn_amd.train_step import FusedTrainStep

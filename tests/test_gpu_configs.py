@@ -22,7 +22,7 @@ import torch
 
 from conftest import ROOT
 from oracle import c_oracle
-from parity import assert_rows_close
+from parity import assert_rows_close, record_stats, trajectory_bar
 
 pytestmark = pytest.mark.gpu
 
@@ -126,13 +126,12 @@ def test_c3_training_step_matches_oracle(gpu, c3, monkeypatch):
         # the same rows move (touched rows and the step's negatives)
         assert np.array_equal(moved_h, moved_r), (name, int(moved_h.sum()), int(moved_r.sum()))
         settled = np.abs(g_r) > 1e-4 * np.abs(g_r).max(axis=1, keepdims=True)
-        diff = np.where(settled, np.abs(ph - pr), 0.0)
-        scale = np.abs(pr).max(axis=1)
-        worst = float((diff.max(axis=1) / np.where(scale > 0, scale, 1.0)).max())
-        assert worst <= 1e-5, (name, worst)
-        noise[name] = (int((~settled & (g_r != 0)).sum()), int((g_r != 0).sum()))
+        # settled elements within 1e-5 of the row's scale; the noise-level ones within 2 lr of the
+        # oracle (one step), their share of the moved elements bounded (tests/parity.py)
+        noise[name] = trajectory_bar(ph, pr, p0, settled, 1e-3, 1, f"C3 {name} end to end")
+    record_stats("c3_training_step", {"loss": loss_a, "loss_oracle": lr_, "grad_row_rel": stats, **noise})
     print(f"C3 batch E={ei_np.shape[1]} f_intra={c3['f_intra']:.4f} loss {loss_a:.7f} vs {lr_:.7f}; "
-          f"grad row-rel {stats}; noise-level gradient elements (unchecked / nonzero) {noise}")
+          f"grad row-rel {stats}; weights {noise}")
 
 
 def _free_port():
@@ -191,12 +190,12 @@ def c5_small(gpu):
     return U, I, ei
 
 
-def test_c5_scaled_forward_matches_oracle(gpu, c5_small, monkeypatch):
+def test_c5_scaled_forward_matches_oracle(gpu, c5_small, tune):
     from lgcn_amd import propagate_forward
     from lgcn_amd.plan import CsrDirection, PropagationPlan
     from lgcn_amd.propagate import lgconv_forward
 
-    monkeypatch.setenv("LGCN_SLICE_MB", "0")  # C5's schedule: slicing is off above 512 MB tables
+    tune(slice_mb=0.0)  # C5's schedule: slicing is off above 512 MB tables
     U, I, ei = c5_small
     N, K, d = U + I, 4, 256
     plan = PropagationPlan(ei, N, side_split=U)

@@ -212,7 +212,7 @@ def _spawn(world, tmp_path, clip, variants, steps=12, npz=None, timeout=300, dev
     tag = "dc" if device_collectives else "h"
     outs = [str(tmp_path / f"w{world}_{tag}_r{r}.pt") for r in range(world)]
     env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", DP_VARIANTS=variants, DP_STEPS=str(steps),
-               OMP_NUM_THREADS="1", LGCN_DEVICE_COLLECTIVES="1" if device_collectives else "0")
+               OMP_NUM_THREADS="1", DP_DEVICE_COLLECTIVES="1" if device_collectives else "0")
     extra = [npz] if npz else []
     procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), str(world), port, outs[r], str(clip), *extra],
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
@@ -266,7 +266,7 @@ def test_column_sharded_graph_replay_matches_eager(gpu, tmp_path, world, clip):
 
 @pytest.mark.parametrize("clip", [float("inf"), 1.0])
 def test_dp_exchanges_device_collectives_equal_host_path(gpu, tmp_path, clip):
-    """Four ranks (gloo, one GPU) down the RCCL branches (LGCN_DEVICE_COLLECTIVES=1: RowExchange's
+    """Four ranks (gloo, one GPU) down the RCCL branches (tuning device_collectives=True: RowExchange's
     all_gather_into_tensor, OwnerExchange's all_to_all_single / all_gather on CUDA tensors,
     ColumnGroup's device all_gather; the capacity all_reduces on device) == the same run through
     host memory, bitwise, for the replicated, owner-sharded and column-sharded modes (eager and

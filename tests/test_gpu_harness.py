@@ -1,5 +1,5 @@
 """The harness's train() (reference utils/train_test.py:66-103) both ways on the GPU: the
-reference-style loop (autograd + torch Adam + clip_grad_norm_, LGCN_HARNESS_FUSED=0) and the fused
+reference-style loop (autograd + torch Adam + clip_grad_norm_, tuning harness_fused=False) and the fused
 batch step it routes to by default (lgcn_amd.harness: HIP forward / BPR / backward, exact row-lazy
 Adam, one hipGraph per batch). Same model init, same seed, so the same negatives: the epoch loss
 within 1e-5, and after every epoch the tables and Adam moments within 1e-5 per row on the elements
@@ -17,6 +17,12 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 
+# the share of moved elements outside the 1e-5 row bar after 4-8 steps of the C3 batches: at most
+# 1.1e-4 in the captured runs (profiles/r05d_parity/: 282 of 2.6M user elements after 8 steps,
+# max |dw| 9.7e-6 against the 2 lr steps = 1.6e-2 allowed) — bound 1e-3, ~9x
+MULTI_STEP_OFF_BAR_FRAC = 1e-3
+
+
 class _Batch:
     def __init__(self, ei):
         self.edge_index = ei
@@ -25,11 +31,11 @@ class _Batch:
         return _Batch(self.edge_index.to(device))
 
 
-def _run(gpu, monkeypatch, fused, U, I, d, init, loader, epochs=2):
+def _run(gpu, tune, fused, U, I, d, init, loader, epochs=2):
     from models.light_gcn import LightGCN
     from utils import train_test as TT
 
-    monkeypatch.setenv("LGCN_HARNESS_FUSED", "1" if fused else "0")
+    tune(harness_fused=bool(fused))
     model = LightGCN(U, I, num_layers=3, dim_h=d).to(gpu)
     with torch.no_grad():
         model.user_embedding.weight.copy_(init[0])
@@ -85,8 +91,8 @@ def _settled(grads, frac=0.05, g_floor=1e-4):
     return ok
 
 
-def _compare(ref, got, grads, w0, what):
-    from parity import assert_rows_close
+def _compare(ref, got, grads, w0, what, lr=1e-3):
+    from parity import assert_rows_close, record_stats, trajectory_bar
 
     n_steps = 0
     for e, (r, g) in enumerate(zip(ref, got)):
@@ -94,38 +100,42 @@ def _compare(ref, got, grads, w0, what):
         assert abs(g["loss"] - r["loss"]) <= 1e-5 * abs(r["loss"]), (e, g["loss"], r["loss"])
         assert g["step"] == r["step"], (g["step"], r["step"])
         n_steps = int(r["step"][0])
-        stats = {}
+        stats = {"loss": g["loss"], "loss_ref": r["loss"]}
         masks = _settled(grads[:n_steps])
         for t, name in enumerate(("user", "item")):
             settled = masks[t]
             # the same rows move
             assert np.array_equal(np.any(g["w"][t] != w0[t], axis=1), np.any(r["w"][t] != w0[t], axis=1)), name
-            for key in ("w", "m"):
-                a, b = g[key][t], r[key][t]
-                diff = np.where(settled, np.abs(a - b), 0.0)
-                scale = np.abs(b).max(axis=1)
-                worst = float((diff.max(axis=1) / np.where(scale > 0, scale, 1.0)).max())
-                assert worst <= 1e-5, (what, e, name, key, worst)
-                stats[f"{name}.{key}"] = worst
+            # weights: settled elements within 1e-5 of their row's scale, every element within
+            # 2 lr per step, the unsettled share of the moved elements bounded (tests/parity.py)
+            stats[f"{name}.w"] = trajectory_bar(g["w"][t], r["w"][t], w0[t], settled, lr, n_steps,
+                                                f"{what} epoch {e} {name} weights")
+            a, b = g["m"][t], r["m"][t]
+            diff = np.where(settled, np.abs(a - b), 0.0)
+            scale = np.abs(b).max(axis=1)
+            worst = float((diff.max(axis=1) / np.where(scale > 0, scale, 1.0)).max())
+            assert worst <= 1e-5, (what, e, name, "m", worst)
+            stats[f"{name}.m_settled_row_rel"] = worst
             # second moments: g^2 sums, no sign question — every row within 1e-5 of its scale
-            assert_rows_close(g["v"][t], r["v"][t], rtol=1e-5, what=f"{what} epoch {e} {name} exp_avg_sq")
-            stats[f"{name}.unsettled"] = int((~settled).sum())
-        print(f"{what} epoch {e}: loss {g['loss']:.8f} vs {r['loss']:.8f}, steps {n_steps}, worst row-rel {stats}")
+            stats[f"{name}.v_row_rel"] = assert_rows_close(g["v"][t], r["v"][t], rtol=1e-5,
+                                                           what=f"{what} epoch {e} {name} exp_avg_sq")[0]
+        record_stats(f"harness_{what.replace(' ', '_')}_epoch{e}", stats)
+        print(f"{what} epoch {e}: loss {g['loss']:.8f} vs {r['loss']:.8f}, steps {n_steps}, {stats}")
 
 
-def test_harness_train_fused_matches_reference_loop_golden(gpu, monkeypatch):
+def test_harness_train_fused_matches_reference_loop_golden(gpu, tune):
     """The golden harness graph's three cluster batches (tests/golden/harness.npz, d = 64)."""
     G = np.load(GOLDEN / "harness.npz")
     U, I = int(G["train_U"]), int(G["train_I"])
     init = (torch.from_numpy(G["train_init_user_w"]), torch.from_numpy(G["train_init_item_w"]))
     loader = [_Batch(torch.from_numpy(G[f"train_batch{p}"])) for p in range(3)]
-    ref, grads = _run(gpu, monkeypatch, False, U, I, 64, init, loader)
-    got, _ = _run(gpu, monkeypatch, True, U, I, 64, init, loader)
+    ref, grads = _run(gpu, tune, False, U, I, 64, init, loader)
+    got, _ = _run(gpu, tune, True, U, I, 64, init, loader)
     w0 = [init[0].numpy(), init[1].numpy()]
     _compare(ref, got, grads, w0, "golden")
 
 
-def test_harness_train_fused_matches_reference_loop_c3(gpu, monkeypatch):
+def test_harness_train_fused_matches_reference_loop_c3(gpu, tune):
     """C3 batches (ML-25M-shaped graph, 1024 parts, 32 parts per batch, K=3, d=128). One step (a
     one-batch epoch): the loss within 1e-5, the tables and both moments per row within 1e-5 on the
     settled elements — test_gpu_configs.py's C3 bar. Four batches, two epochs: every epoch's loss
@@ -143,21 +153,34 @@ def test_harness_train_fused_matches_reference_loop_c3(gpu, monkeypatch):
     init = (torch.randn(U, d) * 0.01, torch.randn(I, d) * 0.01)
     w0 = [init[0].numpy(), init[1].numpy()]
     one = [_Batch(torch.from_numpy(batches[0]))]
-    ref, grads = _run(gpu, monkeypatch, False, U, I, d, init, one, epochs=1)
-    got, _ = _run(gpu, monkeypatch, True, U, I, d, init, one, epochs=1)
+    ref, grads = _run(gpu, tune, False, U, I, d, init, one, epochs=1)
+    got, _ = _run(gpu, tune, True, U, I, d, init, one, epochs=1)
     _compare(ref, got, grads, w0, "C3 one step")
     four = [_Batch(torch.from_numpy(b)) for b in batches[:4]]
-    ref, _ = _run(gpu, monkeypatch, False, U, I, d, init, four, epochs=2)
-    got, _ = _run(gpu, monkeypatch, True, U, I, d, init, four, epochs=2)
+    ref, _ = _run(gpu, tune, False, U, I, d, init, four, epochs=2)
+    got, _ = _run(gpu, tune, True, U, I, d, init, four, epochs=2)
+    from parity import record_stats, trajectory_bar
+
     for e, (r, q) in enumerate(zip(ref, got)):
         assert q["path"] == "fused" and r["path"].startswith("reference")
         assert abs(q["loss"] - r["loss"]) <= 1e-5 * abs(r["loss"]), (e, q["loss"], r["loss"])
         assert q["step"] == r["step"]
-        drift = max(float(np.abs(q["w"][t] - r["w"][t]).max()) for t in range(2))
-        print(f"C3 4 batches, epoch {e}: loss {q['loss']:.8f} vs {r['loss']:.8f}; max |w| difference {drift:.3g}")
+        steps = int(r["step"][0])
+        stats = {"loss": q["loss"], "loss_ref": r["loss"]}
+        for t, name in enumerate(("user", "item")):
+            # after the first step the paths take gradients at weights that already differ where
+            # Adam's sign-like step met a noise-level gradient: here "settled" is simply the
+            # elements inside the 1e-5 row bar, and the share outside it is what is bounded
+            a, b = q["w"][t].astype(np.float64), r["w"][t].astype(np.float64)
+            scale = np.abs(b).max(axis=1, keepdims=True)
+            inside = np.abs(a - b) <= 1e-5 * np.where(scale > 0, scale, 1.0)
+            stats[f"{name}.w"] = trajectory_bar(q["w"][t], r["w"][t], w0[t], inside, 1e-3, steps,
+                                                f"C3 4 batches epoch {e} {name}", max_frac=MULTI_STEP_OFF_BAR_FRAC)
+        record_stats(f"harness_C3_4batches_epoch{e}", stats)
+        print(f"C3 4 batches, epoch {e}: loss {q['loss']:.8f} vs {r['loss']:.8f}; {stats}")
 
 
-def test_harness_train_falls_back(gpu, monkeypatch):
+def test_harness_train_falls_back(gpu, tune):
     """What the fused step does not reproduce runs the reference loop (and says why)."""
     from models.light_gcn import LightGCN
     from utils import train_test as TT
@@ -173,3 +196,88 @@ def test_harness_train_falls_back(gpu, monkeypatch):
     bad = [_Batch(torch.tensor([[0, U], [1, U + 1]]))]  # a user-user and an item-item edge: not bipartite
     TT.train(model, torch.optim.Adam(model.parameters(), lr=1e-3), bad, gpu)
     assert TT.LAST_TRAIN_PATH.startswith("reference") and "bipartite" in TT.LAST_TRAIN_PATH
+
+
+class _FreshLoader:
+    """Collates a new edge_index tensor on every iteration, as the reference's PyG
+    DataLoader(batch_size=1, shuffle=True) does (reference data/dataset_handler.py:285)."""
+
+    def __init__(self, arrays):
+        self.arrays = arrays
+
+    def __len__(self):
+        return len(self.arrays)
+
+    def __iter__(self):
+        for a in self.arrays:
+            yield _Batch(torch.from_numpy(a.copy()))
+
+
+def _epochs(gpu, U, I, init, loader, epochs):
+    from lgcn_amd import harness
+    from models.light_gcn import LightGCN
+    from utils import train_test as TT
+
+    model = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
+    with torch.no_grad():
+        model.user_embedding.weight.copy_(init[0])
+        model.item_embedding.weight.copy_(init[1])
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    torch.manual_seed(41)
+    losses, mem = [], []
+    for _ in range(epochs):
+        losses.append(TT.train(model, opt, loader, gpu))
+        assert TT.LAST_TRAIN_PATH == "fused", TT.LAST_TRAIN_PATH
+        torch.cuda.synchronize()
+        mem.append(torch.cuda.memory_allocated(gpu))
+    w = [model.user_embedding.weight.detach().cpu().clone(), model.item_embedding.weight.detach().cpu().clone()]
+    return losses, w, harness._FAST[opt], mem
+
+
+def test_harness_fresh_tensors_each_epoch_replay(gpu, tune):
+    """a loader that collates new edge_index tensors every epoch finds each
+    batch's state (plans, captured hipGraph) by content — bitwise the same run as a loader that
+    yields the same objects, one state per distinct batch, no memory growth across epochs."""
+    tune(harness_fused=True)
+    G = np.load(GOLDEN / "harness.npz")
+    U, I = int(G["train_U"]), int(G["train_I"])
+    init = (torch.from_numpy(G["train_init_user_w"]), torch.from_numpy(G["train_init_item_w"]))
+    arrays = [G[f"train_batch{p}"] for p in range(3)]
+    same = [_Batch(torch.from_numpy(a)) for a in arrays]
+    l_same, w_same, _, _ = _epochs(gpu, U, I, init, same, 4)
+    l_fresh, w_fresh, fast, mem = _epochs(gpu, U, I, init, _FreshLoader(arrays), 4)
+    assert l_same == l_fresh, (l_same, l_fresh)
+    for a, b in zip(w_same, w_fresh):
+        assert torch.equal(a, b)
+    states = fast.step._states
+    assert len(states) == 3, len(states)
+    assert states.misses == 3 and states.hits_content + states.hits_object >= 9, \
+        (states.misses, states.hits_content, states.hits_object)
+    assert all(getattr(st, "graph", None) is not None for st in states.values())  # captured, replayed
+    assert mem[1] == mem[2] == mem[3], mem
+
+
+def test_harness_one_shot_loader_falls_back_mid_epoch(gpu, tune):
+    """a non-bipartite batch after fused steps hands the rest of the epoch to the
+    reference loop — the fused steps' Adam state written back first, no batch lost from a one-shot
+    iterator (4 batches -> 4 Adam steps in the torch optimizer)."""
+    from models.light_gcn import LightGCN
+    from utils import train_test as TT
+
+    tune(harness_fused=True)
+    G = np.load(GOLDEN / "harness.npz")
+    U, I = int(G["train_U"]), int(G["train_I"])
+    good = [_Batch(torch.from_numpy(G[f"train_batch{p}"])) for p in range(3)]
+    bad = _Batch(torch.tensor([[0, U], [1, U + 1]]))
+    model = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    loss = TT.train(model, opt, iter([good[0], good[1], bad, good[2]]), gpu)
+    assert np.isfinite(loss)
+    assert TT.LAST_TRAIN_PATH.startswith("reference: fused for 2 batch(es)"), TT.LAST_TRAIN_PATH
+    for p in (model.user_embedding.weight, model.item_embedding.weight):
+        assert int(float(opt.state[p]["step"])) == 4
+    # the next epoch starts fused again from the written-back state
+    TT.train(model, opt, good, gpu)
+    assert TT.LAST_TRAIN_PATH == "fused"
+    for p in (model.user_embedding.weight, model.item_embedding.weight):
+        assert int(float(opt.state[p]["step"])) == 7

@@ -44,14 +44,14 @@ def _pass(direction, x, y, acc, part, mode, e=None, div=1.0, mul=1.0, packed=Fal
 @pytest.mark.parametrize("chunk,xcd,packed", [(8, "0", False), (4096, "0", False), (8, "4", False),
                                               (4096, "4", False), (8, "4", True), (2, "4", True), (8, "3", True),
                                               (8, "7", False)])
-def test_spmm_pair_bitwise_single_passes(gpu, monkeypatch, d, chunk, xcd, packed):
-    """xcd = LGCN_PAIR_XCD: the XCD-split block mapping (pass a on xcd of the 8 XCDs, b on the rest,
+def test_spmm_pair_bitwise_single_passes(gpu, tune, d, chunk, xcd, packed):
+    """xcd = tuning pair_xcds_a: the XCD-split block mapping (pass a on xcd of the 8 XCDs, b on the rest,
     while both have blocks left; 0 = a's blocks then b's) gives the same rows; packed: split rows ordered big-first (pack_split_rows) and the
     <= 16-chunk ones combined one per lane group — the same rows too (chunk 2: hub rows of
     hundreds of chunks beside small ones)."""
     import graphs
 
-    monkeypatch.setenv("LGCN_PAIR_XCD", xcd)
+    tune(pair_xcds_a=int(xcd))
     from lgcn_amd import _ffi
     from lgcn_amd.plan import pack_split_rows
     from lgcn_amd.propagate import spmm
@@ -248,3 +248,33 @@ def test_spmm_pass_bitwise_spmm(gpu, d, chunk, packed):
             outs.append((acc.cpu(), y.cpu()))
         for got in outs[1:]:
             assert torch.equal(got[0], outs[0][0]) and torch.equal(got[1], outs[0][1]), mode
+
+
+@pytest.mark.parametrize("d", [4, 16, 64, 256, 1024])
+def test_spmm_pass_small_row_combine_outside_contract(gpu, d):
+    """every split row handed to the one-per-lane-group combine (n_split_big = 0,
+    with hub rows of hundreds of chunks among them, no pack_split_rows) is still combined in
+    combine_row's association — bitwise lgcn_spmm's rows."""
+    import graphs
+
+    from lgcn_amd import _ffi
+    from lgcn_amd.propagate import spmm
+
+    U, I, ei = graphs.hub(U=1500, I=40, seed=1)
+    N = U + I
+    da = _direction(gpu, ei, N, 2, U)
+    pc = da.splits[:da.n_splits, 2].cpu()
+    assert int(pc.max()) > 16 and int(pc.min()) <= 16  # big and small rows both
+    g = torch.Generator(device=gpu).manual_seed(d)
+    x = torch.randn(N, d, device=gpu, generator=g)
+    part = torch.empty((max(1, da.n_partials), d), device=gpu)
+    lib = _ffi.load()
+    acc0 = torch.full((N, d), 0.5, device=gpu)
+    spmm(da, N, d, (x, None, N), None, (acc0, None, N), None, _ffi.EPI_STORE, 1.0, 1.0, part)
+    acc1 = torch.full((N, d), 0.5, device=gpu)
+    p = _ffi.Pass(da.items.data_ptr(), da.n_items, da.splits.data_ptr(), da.n_splits, da.col.data_ptr(),
+                  da.val.data_ptr(), x.data_ptr(), None, N, None, None, N, None, acc1.data_ptr(), None, N,
+                  part.data_ptr(), _ffi.EPI_STORE, 1.0, 1.0, n_split_big=0)
+    _ffi.check(lib.lgcn_spmm_pass(ctypes.byref(p), N, d, 3, _ffi.stream_of(gpu)), "pass")
+    torch.cuda.synchronize()
+    assert torch.equal(acc0.cpu(), acc1.cpu())

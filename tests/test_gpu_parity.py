@@ -112,14 +112,14 @@ def test_bit_exact_unsplit(gpu, name):
 
 
 @pytest.mark.parametrize("d", [4, 16, 64, 128, 256, 512, 1024])
-@pytest.mark.parametrize("variant", ["2", "3"])
-def test_tail_paths_bit_exact(gpu, monkeypatch, d, variant):
-    """Both item-pass tail paths (LGCN_SPMM_VARIANT 2 = predicated tail forced on, 3 = forced
+@pytest.mark.parametrize("tail", [1, 0])
+def test_tail_paths_bit_exact(gpu, tune, d, tail):
+    """Both item-pass tail paths (tuning spmm_tail 1 = predicated tail forced on, 0 = forced
     off; the default picks per width and launch size) add in CSR order: unsplit rows of every
     length 1..max are bitwise the oracle, forward and backward."""
     from lgcn_amd import propagate_backward, propagate_forward
 
-    monkeypatch.setenv("LGCN_SPMM_VARIANT", variant)
+    tune(spmm_tail=tail)
     U, I, ei = graphs.sym()
     N, K = U + I, 2
     plan = _plan(ei, N, gpu, chunk=1 << 20)

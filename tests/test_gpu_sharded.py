@@ -17,7 +17,7 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-# (graph, K, d, chunk, LGCN_SLICE_MB or None)
+# (graph, K, d, chunk, tuning slice_mb or None)
 CASES = {
     "ml25m5_plain": ("ml25m", 3, 64, 256, None),
     "ml25m5_sliced": ("ml25m", 3, 64, 64, "0.7"),
@@ -51,22 +51,16 @@ def _reference(dev, case, R=1, F=1):
     import graphs
 
     uw, iw = graphs.embeddings(U, I, d, seed=K + d)
-    saved = os.environ.get("LGCN_SLICE_MB")
-    if R > 1:
-        os.environ["LGCN_SLICE_MB"] = "0"
+    from lgcn_amd import tuning
+
     Fw = F if R == 1 else 1
     w = d // Fw
-    try:
+    with tuning.tuned(**({"slice_mb": 0.0} if R > 1 else {})):
         plan = PropagationPlan(torch.from_numpy(ei).to(dev), U + I, rank_chunk(chunk, R), side_split=U)
         outs = [propagate_forward(torch.from_numpy(uw[:, c * w:(c + 1) * w].copy()).to(dev),
                                   torch.from_numpy(iw[:, c * w:(c + 1) * w].copy()).to(dev), plan, K).cpu().numpy()
                 for c in range(Fw)]
         sched = plan.schedule("fwd", w)
-    finally:
-        if saved is None:
-            os.environ.pop("LGCN_SLICE_MB", None)
-        else:
-            os.environ["LGCN_SLICE_MB"] = saved
     return U, I, ei, uw, iw, np.concatenate(outs, axis=1), sched, F * sched.n_splits
 
 
@@ -95,10 +89,10 @@ def _sharded(dev, case, world, rank, F=1, mode="allgather"):
 
 
 @pytest.mark.parametrize("case", list(CASES))
-def test_sharded_w1_bitwise(gpu, monkeypatch, case):
+def test_sharded_w1_bitwise(gpu, tune, case):
     slice_mb = CASES[case][4]
     if slice_mb:
-        monkeypatch.setenv("LGCN_SLICE_MB", slice_mb)
+        tune(slice_mb=float(slice_mb))
     U, I, ei, uw, iw, ref, sched, _ = _reference(gpu, case)
     shards, splan, ou, oi = _sharded(gpu, case, 1, 0)
     assert shards.NP == U + I and splan.sliced == hasattr(sched, "launches")
@@ -121,11 +115,13 @@ def _worker(rank, world, port, case, out_dir, F=1, mode="allgather", dc=False):
     sys.path[:0] = [str(PKG), str(ROOT), str(ROOT / "tests")]
     import torch.distributed as dist
 
+    from lgcn_amd import tuning
+
     slice_mb = CASES[case][4]
     if slice_mb:
-        os.environ["LGCN_SLICE_MB"] = slice_mb
+        tuning.set_tuning(slice_mb=float(slice_mb))
     if dc:  # the RCCL branch's code (side stream, events, in-place device collectives) over gloo
-        os.environ["LGCN_DEVICE_COLLECTIVES"] = "1"
+        tuning.set_tuning(device_collectives=True)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -145,27 +141,27 @@ def _worker(rank, world, port, case, out_dir, F=1, mode="allgather", dc=False):
                          [("ml25m5_sliced", 2, 2, "allgather"), ("hub_sliced", 2, 2, "allgather"),
                           ("ml25m5_sliced", 4, 2, "allgather"), ("sub_K2_d128", 4, 2, "allgather"),
                           ("ml25m5_plain", 3, 1, "p2p"), ("hub_sliced", 4, 2, "p2p")])
-def test_sharded_ranks_bitwise(gpu, monkeypatch, tmp_path, case, world, F, mode):
+def test_sharded_ranks_bitwise(gpu, tune, tmp_path, case, world, F, mode):
     """world / F row groups x F column groups (gloo, every rank on the one GPU): the assembled
     output is bitwise the one-GPU forward with the schedule the ranks run (R = 1: each column share
     at its width; R > 1: lgcn_amd.sharded.rank_chunk at the full width); with R > 1 also within
     1e-5 per row of the default one."""
-    _check_sharded_ranks(gpu, monkeypatch, tmp_path, case, world, F, mode, False)
+    _check_sharded_ranks(gpu, tune, tmp_path, case, world, F, mode, False)
 
 
 @pytest.mark.parametrize("case,world,F,mode", [("ml25m5_sliced", 4, 2, "allgather"), ("hub_sliced", 4, 2, "p2p"),
                                                ("ml25m5_plain", 3, 1, "p2p"), ("sub_K2_d128", 2, 1, "allgather")])
-def test_sharded_ranks_device_collectives(gpu, monkeypatch, tmp_path, case, world, F, mode):
-    """The same, down the RCCL branch of BlockExchange (LGCN_DEVICE_COLLECTIVES=1: in-place
+def test_sharded_ranks_device_collectives(gpu, tune, tmp_path, case, world, F, mode):
+    """The same, down the RCCL branch of BlockExchange (tuning device_collectives=True: in-place
     all_gather_into_tensor / batch_isend_irecv on CUDA tensors, on a side stream the compute
     stream waits on through events), with gloo carrying the bytes: bitwise the one-GPU forward."""
-    _check_sharded_ranks(gpu, monkeypatch, tmp_path, case, world, F, mode, True)
+    _check_sharded_ranks(gpu, tune, tmp_path, case, world, F, mode, True)
 
 
-def _check_sharded_ranks(gpu, monkeypatch, tmp_path, case, world, F, mode, dc):
+def _check_sharded_ranks(gpu, tune, tmp_path, case, world, F, mode, dc):
     slice_mb = CASES[case][4]
     if slice_mb:
-        monkeypatch.setenv("LGCN_SLICE_MB", slice_mb)
+        tune(slice_mb=float(slice_mb))
     R = world // F
     U, I, ei, uw, iw, ref, sched, n_hubs = _reference(gpu, case, R, F)
     torch.cuda.synchronize()
@@ -194,7 +190,9 @@ def _reduce_worker(rank, world, port, case, out_dir, F=1, dc=False, fused=False)
     import torch.distributed as dist
 
     if dc:
-        os.environ["LGCN_DEVICE_COLLECTIVES"] = "1"
+        from lgcn_amd import tuning
+
+        tuning.set_tuning(device_collectives=True)
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -233,7 +231,7 @@ def test_reduce_mode_ranks_match_oracle(gpu, tmp_path, case, world, F):
 
 @pytest.mark.parametrize("case,world,F", [("ml25m5_plain", 4, 2), ("ml25m5_sliced", 8, 2), ("hub_sliced", 3, 1)])
 def test_reduce_mode_device_collectives(gpu, tmp_path, case, world, F):
-    """The same down ItemReducer's RCCL branch (LGCN_DEVICE_COLLECTIVES=1: all_reduce and the last
+    """The same down ItemReducer's RCCL branch (tuning device_collectives=True: all_reduce and the last
     layer's reduce_scatter_tensor on CUDA tensors, side stream + events), gloo carrying the bytes."""
     _check_reduce_ranks(gpu, tmp_path, case, world, F, True)
 

@@ -1,6 +1,6 @@
 """The source-sliced schedule (lgcn_amd.sliced, lgcn_spmm_run): one launch per source slice,
 row sums carried between launches through the running buffer. Forced on small graphs with
-LGCN_SLICE_MB and a short chunk (so hub rows take the chunk + combine path too), against the C
+tuning slice_mb and a short chunk (so hub rows take the chunk + combine path too), against the C
 oracle: within 1e-5 everywhere, and bitwise on every row summed as one sequential chain."""
 import numpy as np
 import pytest
@@ -20,9 +20,9 @@ def _plan(ei, N, dev, U, chunk):
 
 
 @pytest.fixture
-def force_slices(monkeypatch):
+def force_slices(tune):
     def set_mb(mb):
-        monkeypatch.setenv("LGCN_SLICE_MB", str(mb))
+        tune(slice_mb=float(mb))
     return set_mb
 
 
@@ -149,11 +149,10 @@ def test_uncoalesced_edges_fall_back_to_plain_schedule(gpu, force_slices):
 
 
 
-@pytest.mark.parametrize("d,cms", [(64, ["1", "2", "4"]), (32, ["1", "4", "8"]), (16, ["2", "8", "16"]),
-                                   (8, ["4", "16", "32"])])
+@pytest.mark.parametrize("d,cms", [(64, [1, 2, 4]), (32, [1, 4, 8]), (16, [2, 8, 16]), (8, [4, 16, 32])])
 @pytest.mark.parametrize("sliced", [True, False])
-def test_index_rounds_bitwise(gpu, force_slices, monkeypatch, d, cms, sliced):
-    """Index load rounds (LGCN_SPMM_CM batches of col/val per load round) only change how many
+def test_index_rounds_bitwise(gpu, force_slices, tune, d, cms, sliced):
+    """Index load rounds (tuning spmm_index_rounds batches of col/val per load round) only change how many
     indices a lane group loads at once, never the adds: every round size gives the same floats,
     on the sliced and the plain schedule, and matches the oracle."""
     from lgcn_amd.propagate import lgconv_forward
@@ -165,7 +164,7 @@ def test_index_rounds_bitwise(gpu, force_slices, monkeypatch, d, cms, sliced):
     x = torch.from_numpy(np.random.default_rng(d).standard_normal((N, d)).astype(np.float32)).to(gpu)
     outs = []
     for cm in cms:
-        monkeypatch.setenv("LGCN_SPMM_CM", cm)
+        tune(spmm_index_rounds=cm)
         outs.append(lgconv_forward(x, plan).cpu().numpy())
     for o in outs[1:]:
         assert np.array_equal(o, outs[0])
@@ -175,7 +174,7 @@ def test_index_rounds_bitwise(gpu, force_slices, monkeypatch, d, cms, sliced):
 
 @pytest.mark.parametrize("name", ["sym", "subsampled", "hub"])
 @pytest.mark.parametrize("K,d,mb", [(2, 64, 0.005), (3, 64, 0.01), (4, 16, 0.002), (5, 128, 0.02), (3, 256, 0.05)])
-def test_sliced_ride_bitwise(gpu, force_slices, monkeypatch, name, K, d, mb):
+def test_sliced_ride_bitwise(gpu, force_slices, tune, name, K, d, mb):
     """The riding-combine forward (lgcn_spmm_run_slices_ride: slice groups alternating per layer,
     each group's split rows combined inside the next group's first launch, partials double-buffered
     by layer parity, one combine launch at the end) is bitwise the per-layer slices + combine — run
@@ -193,9 +192,9 @@ def test_sliced_ride_bitwise(gpu, force_slices, monkeypatch, name, K, d, mb):
     assert r["users"][1] + r["items"][1] == sched.n_splits
     uw, iw = graphs.embeddings(U, I, d, seed=K + d)
     uw_t, iw_t = torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu)
-    monkeypatch.setenv("LGCN_SLICE_RIDE", "0")
+    tune(slice_ride=False)
     want = propagate_forward(uw_t, iw_t, plan, K).cpu()
-    monkeypatch.setenv("LGCN_SLICE_RIDE", "1")
+    tune(slice_ride=True)
     for _ in range(2):
         got = propagate_forward(uw_t, iw_t, plan, K).cpu()
         assert torch.equal(got, want)

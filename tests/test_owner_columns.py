@@ -119,16 +119,17 @@ def _dc_worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from lgcn_amd.distributed import device_collectives
 
+    from lgcn_amd import tuning
+
     plain = device_collectives()
-    os.environ["LGCN_DEVICE_COLLECTIVES"] = "1"
-    forced = device_collectives()
-    os.environ.pop("LGCN_DEVICE_COLLECTIVES")
+    with tuning.tuned(device_collectives=True):
+        forced = device_collectives()
     torch.save({"plain": plain, "forced": forced}, os.path.join(out, f"dc{rank}.pt"))
     dist.destroy_process_group()
 
 
 def test_device_collectives_switch(tmp_path):
-    """device_collectives(): False on a gloo group, True with LGCN_DEVICE_COLLECTIVES=1 (how the
+    """device_collectives(): False on a gloo group, True with tuning device_collectives=True (how the
     GPU tests send gloo runs down the RCCL branches)."""
     mp.spawn(_dc_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     for r in range(2):

@@ -31,14 +31,14 @@ def test_legacy_choice_errors_like_numpy():
         legacy_choice(5, 6, 1)
 
 
-@pytest.mark.parametrize("threads", ["1", "2", "3", "16"])
-def test_legacy_choice_parallel_draws_match_numpy(monkeypatch, threads):
+@pytest.mark.parametrize("threads", [1, 2, 3, 16])
+def test_legacy_choice_parallel_draws_match_numpy(tune, threads):
     """The evaluate() shape (10 draws of 100 from 621,562): draws run on worker threads from the
     states the main thread's accept-test walk hands them; any thread count gives numpy's picks
     and numpy's final state."""
     from lgcn_amd.recall import legacy_choice
 
-    monkeypatch.setenv("LGCN_CHOICE_THREADS", threads)
+    tune(choice_threads=threads)
     np.random.seed(11)
     np.random.random(3)
     got = legacy_choice(621562, 100, 10)

@@ -77,10 +77,12 @@ def main():
                     nb[id(dr)] = dr.n_split_big
                     if unpacked:
                         dr.n_split_big = -1
-                # fused-seq: the pair launch without its XCD-split block mapping (LGCN_PAIR_XCD=0);
+                # fused-seq: the pair launch without its XCD-split block mapping (pair_xcds_a=0);
                 # fusedN: pass a (the item partials) on N of the 8 XCDs
-                os.environ["LGCN_PAIR_XCD"] = ("0" if order == "fused-seq" else
-                                               order[5:] if order[5:].isdigit() else "4")
+                from lgcn_amd import tuning
+
+                tuning.set_tuning(pair_xcds_a=0 if order == "fused-seq" else
+                                  int(order[5:]) if order[5:].isdigit() else 4)
                 with torch.no_grad():
                     for _ in range(3):
                         propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)

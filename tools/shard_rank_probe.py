@@ -21,11 +21,13 @@ def main():
     ap.add_argument("--grids", default="1x1,2x1,4x1,8x1,1x2,2x2,4x2,2x4")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--chunks", default="256")
-    ap.add_argument("--plain", action="store_true", help="LGCN_SLICE_MB=0: the plain item schedule")
+    ap.add_argument("--plain", action="store_true", help="tuning slice_mb=0: the plain item schedule")
     ap.add_argument("--full-slices", action="store_true", help="R = 1 ranks keep the full width's slices")
     args = ap.parse_args()
     if args.plain:
-        os.environ["LGCN_SLICE_MB"] = "0"
+        from lgcn_amd import tuning
+
+        tuning.set_tuning(slice_mb=0.0)
     dev = torch.device("cuda")
     g = synth.ml25m_shaped(seed=0)
     U, I, N, E = g.num_users, g.num_items, g.num_nodes, g.num_edges
