@@ -16,7 +16,6 @@ the union of the ranks' rows.
 """
 from __future__ import annotations
 
-
 import torch
 import torch.distributed as dist
 
