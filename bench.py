@@ -1028,9 +1028,10 @@ def run_train(args):
     def step(bidx, nxt=None):
         batch = batches[bidx]
         if fused is not None:
-            # next batch: owner mode fetches its rows; the single-GPU / column-sharded row-lazy step
-            # runs its users' Adam catch-up inside this step's launches (FusedTrainStep._ride)
-            fused.step(batch, batches[nxt] if nxt is not None else None)
+            if dp_mode == "owner":
+                fused.step(batch, batches[nxt] if nxt is not None else None)
+            else:
+                fused.step(batch)
             return batch.edge_index.shape[1]
         opt.zero_grad()
         loss = bpr_loss(*compute_embeddings(model, batch, dev))
@@ -1046,9 +1047,8 @@ def run_train(args):
              D.rank_share(len(batches), world, rank, seed=0, epoch=0))
 
     def nxt_of(i, last):
-        """the batch index of step i + 1 (owner mode fetches its rows; the row-lazy step rides its
-        users' catch-up), None after an epoch's end (sync() makes every row current there) or the
-        run's last step"""
+        """the batch index of step i + 1 (owner mode fetches its rows), None after an epoch's end
+        (sync() makes every row current there) or the run's last step"""
         return None if (i + 1) % len(share) == 0 or i + 1 == last else share[(i + 1) % len(share)]
 
     n_warm = max(args.warmup, 2 * len(share))

@@ -284,47 +284,11 @@ int lgcn_spmm_run_slices(const lgcn_item_t* items, const int64_t* slice_offsets,
  * g, g+G, ... then the G group sums in order), so the result is bitwise lgcn_spmm's; `partial`
  * is unused (may be NULL). Vector widths only (d in {4, 8, ..., 1024}, 16-byte aligned rows).
  * Replaces the same reference code as lgcn_spmm (models/light_gcn.py:33, LGConv.propagate). */
-/* The Adam catch-up that rides in a block-split launch (ABI 7): extra workgroups of the launch
- * advance rows[0, n_rows) — rows whose gradient in the step in progress is zero (the caller's
- * contract: a Cluster-GCN batch's users are touched only by that batch, so the NEXT batch's users
- * qualify, minus any the current batch touches: skip[row] != 0 leaves a row alone) — by at most
- * max_replays zero-gradient Adam steps each, from last[row] + 1 up to step[0] + 1 (the step in
- * progress: step[0] counts completed steps), with lgcn_row_adam's arithmetic (so bitwise the
- * catch-up the row would get later), and set last[row]. Replays spread over a step's launches
- * run on CUs its latency-bound passes leave idle; the next step's catch-up finds those rows
- * current. Tables and consts as lgcn_row_adam's; d is the launch's d. */
-typedef struct {
-    const int32_t* rows;
-    int64_t n_rows;
-    const uint8_t* skip; /* nullable */
-    float* p_lo;
-    float* p_hi;
-    float* m_lo;
-    float* m_hi;
-    float* v_lo;
-    float* v_hi;
-    int64_t split;
-    int32_t* last;
-    const int64_t* step;
-    const float* consts;
-    float one_minus_beta1;
-    float beta2;
-    float eps;
-    int32_t max_replays;
-} lgcn_adam_ride_t;
-
 int lgcn_spmm_blocksplit(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* splits, int64_t n_splits,
                          const int32_t* col, const float* val, int64_t N, int32_t d, const float* x_lo,
                          const float* x_hi, int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split,
                          float* y, float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
                          float div, float mul, lgcn_stream_t stream, const lgcn_item_t* chunks);
-/* lgcn_spmm_blocksplit with a riding Adam catch-up (ride may be NULL: the plain call). */
-int lgcn_spmm_blocksplit_ride(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* splits, int64_t n_splits,
-                              const int32_t* col, const float* val, int64_t N, int32_t d, const float* x_lo,
-                              const float* x_hi, int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split,
-                              float* y, float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
-                              float div, float mul, lgcn_stream_t stream, const lgcn_item_t* chunks,
-                              const lgcn_adam_ride_t* ride);
 
 /* Two independent plain passes of one width d over N-row tables, each described by the arguments
  * lgcn_spmm takes (lgcn_pass_t below), issued together: what = 1 runs both item passes in ONE

@@ -48,9 +48,33 @@ struct RowList {
     const uint8_t* skip_b;   // nullable: ... and !skip_b[row] (the row is already in list a)
 };
 
+struct AdamK {
+    float omb1, beta2, omb2, eps;
+    int markstein;  // the step-constant division by Markstein's correction (div_step)
+};
+
 template <class T>
 __device__ __forceinline__ T* trow(T* lo, T* hi, int64_t split, int64_t r, int64_t d) {
     return r < split ? lo + r * d : hi + (r - split) * d;
+}
+
+// sqrt(v) / c with c = bc2_sqrt, the step's constant, and rc = 1 / c (both fp32, rc correctly
+// rounded): Markstein's correction q0 = s * rc, r = fma(-c, q0, s) (exact), q = fma(r, rc, q0)
+// gives the correctly rounded quotient — the value IEEE division gives — in 3 instructions instead
+// of the division's 9 (v_div_scale x 2, v_rcp, 4 FMAs, v_div_fmas, v_div_fixup). Proven for the
+// schedule of beta2 = 0.999 (the reference's Adam default): tools/markstein_check.c tries every
+// significand of a binade — by scale invariance every normal s; s = sqrt(v) is never subnormal —
+// for each of its 10,030 distinct step constants, 0 mismatches (profiles/r03x_adam/). The proof
+// covers the constants built from the double beta2 = 0.999 exactly: lgcn_adam_consts records that in
+// consts[0].x (kConstsMarkstein), and k_row_adam takes the shortcut only when it is set; any other
+// beta2 — np.float32(0.999) passed as a double included — takes the IEEE division. That the device's
+// constants equal the checker's host-libm ones is a GPU test (test_gpu_training.py).
+__device__ __forceinline__ float div_step(float s, float c, float rc, int markstein) {
+    if (markstein) {
+        const float q0 = s * rc;
+        return __builtin_fmaf(__builtin_fmaf(-c, q0, s), rc, q0);
+    }
+    return s / c;
 }
 
 // the dense kernel's element update (lgcn_optim.hip adam_elem), verbatim
@@ -60,6 +84,17 @@ __device__ __forceinline__ void adam_elem(float& p, float& g, float& m, float& v
     m = m + k.omb1 * (g - m);
     v = v * k.beta2;
     v = v + k.omb2 * (g * g);
+    const float denom = div_step(sqrtf(v), bc2_sqrt, rc, k.markstein) + k.eps;
+    p = p + step_size * (m / denom);
+}
+
+// adam_elem with g == 0 (a missed step), the same floats with fewer instructions: g * coef and
+// g * g are +0, so v + omb2 * 0 == v * beta2 (v >= 0 and omb2 finite: adding +0 changes nothing),
+// and m + omb1 * (0 - m) == m - omb1 * m (0 - m == -m exactly for m != 0, m is never -0).
+__device__ __forceinline__ void adam_elem_zero(float& p, float& m, float& v, float step_size, float bc2_sqrt,
+                                               float rc, const AdamK& k) {
+    m = m - k.omb1 * m;
+    v = v * k.beta2;
     const float denom = div_step(sqrtf(v), bc2_sqrt, rc, k.markstein) + k.eps;
     p = p + step_size * (m / denom);
 }

@@ -57,8 +57,6 @@ struct SpmmArgs {
     // combine launches: split rows [0, n_big) get a workgroup each; rows [n_big, n_splits) have at
     // most kVSums chunks and are combined one per lane group (lgcn_spmm_pair's n_split_big)
     int64_t n_big = -1;  // -1: every split row gets a workgroup
-    // block-split launches: the Adam catch-up riding in extra workgroups (host-side; lgcn_adam_ride_t)
-    const lgcn_adam_ride_t* ride = nullptr;
 };
 
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -380,22 +378,6 @@ __global__ __launch_bounds__(kBlock) void k_spmm_vec(SpmmArgs a) {
     item_pass<LPR, NV, UNROLL, SLICED, TAIL, BSPLIT, CM>(a, blockIdx.x);
 }
 
-// A block-split launch (lgcn_spmm_blocksplit_ride) whose workgroups [main_blocks, grid) carry the
-// riding Adam catch-up: one ride entry per lane group. Those workgroups touch no row, y, acc or
-// partial of the pass (disjoint data: the optimizer's p / m / v / last of rows the step does not
-// touch), so the pass's rows are bitwise the plain launch's; a small batch's pass leaves most CUs
-// idle while its longest chains finish, and the replays fill them.
-template <int LPR, int NV, int UNROLL, int TAIL, int CM>
-__global__ __launch_bounds__(kBlock) void k_spmm_bsplit_ride(SpmmArgs a, AdamRide r, int64_t main_blocks) {
-    if (int64_t(blockIdx.x) >= main_blocks) {
-        constexpr int GPB = kBlock / LPR;
-        adam_ride_entry<LPR, NV>(r, (int64_t(blockIdx.x) - main_blocks) * GPB + threadIdx.x / LPR,
-                                 threadIdx.x % LPR);
-        return;
-    }
-    item_pass<LPR, NV, UNROLL, false, TAIL, true, CM>(a, blockIdx.x);
-}
-
 // Two independent plain item passes of one width in one launch (lgcn_spmm_pair): workgroups
 // [0, blocks_a) run pass a, the rest pass b. Each pass keeps its own longest-first order, and b's
 // longest items start while a's last workgroups drain, so the pair pays one launch gap and one
@@ -699,17 +681,6 @@ int launch_vec(const SpmmArgs& a, hipStream_t s, int pass, const SpmmArgs* b = n
     }
     if (pass == PASS_BSPLIT) {  // split rows (one workgroup each) and items in one launch
         const int64_t blocks = a.n_splits + (a.n_items + GPB - 1) / GPB;
-        const int64_t rb = a.ride ? (a.ride->n_rows + GPB - 1) / GPB : 0;
-        if (rb > 0) {
-            const lgcn_adam_ride_t& q = *a.ride;
-            const AdamRide r{q.rows, q.n_rows, q.skip, q.p_lo, q.p_hi, q.m_lo, q.m_hi, q.v_lo, q.v_hi, q.split,
-                             q.last, q.step, reinterpret_cast<const float4*>(q.consts),
-                             AdamK{q.one_minus_beta1, q.beta2, 0.0f, q.eps, q.beta2 == 0.999f ? 1 : 0},
-                             q.max_replays};
-            k_spmm_bsplit_ride<LPR, NV, UNROLL, TAIL, CM><<<dim3(static_cast<unsigned>(blocks + rb)), kBlock, 0, s>>>(
-                a, r, blocks);
-            return check_launch("k_spmm_bsplit_ride");
-        }
         if (blocks > 0) {
             k_spmm_vec<LPR, NV, UNROLL, false, TAIL, true, CM><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(a);
             if (int rc = check_launch("k_spmm_vec")) return rc;
@@ -828,27 +799,13 @@ int spmm_impl(const lgcn_item_t* items, int64_t n_items, const lgcn_split_t* spl
               const float* x_hi, int64_t x_split, const float* e_lo, const float* e_hi, int64_t e_split,
               float* y, float* acc_lo, float* acc_hi, int64_t acc_split, float* partial, int32_t mode,
               float div, float mul, lgcn_stream_t stream, int pass, float* run = nullptr,
-              const lgcn_item_t* chunks = nullptr, const lgcn_adam_ride_t* ride = nullptr) {
+              const lgcn_item_t* chunks = nullptr) {
     if (int rc = check_pass(items, n_items, splits, n_splits, N, d, x_lo, x_hi, x_split, e_lo, e_hi, e_split, acc_lo,
                             acc_hi, acc_split, partial, mode, pass, chunks))
         return rc;
-    if (ride != nullptr && ride->n_rows > 0) {
-        const lgcn_adam_ride_t& q = *ride;
-        if (!q.rows || !q.p_lo || !q.m_lo || !q.v_lo || !q.last || !q.step || !q.consts || q.split < 0 ||
-            q.max_replays < 0 || (q.split < N && (!q.p_hi || !q.m_hi || !q.v_hi)))
-            return fail(LGCN_E_ARG, "lgcn_spmm_blocksplit_ride: bad ride");
-        const void* ps[] = {q.p_lo, q.p_hi, q.m_lo, q.m_hi, q.v_lo, q.v_hi, q.consts};
-        for (const void* p : ps)
-            if (p && !aligned16(p)) return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm_blocksplit_ride: ride tables alignment");
-        if (d % 4 || d > 1024 || (d & (d - 1)))
-            return fail(LGCN_E_UNSUPPORTED, "lgcn_spmm_blocksplit_ride: d=%d (the ride needs a vector width)", d);
-    } else {
-        ride = nullptr;
-    }
-    if (N == 0 || ((n_items == 0 && n_splits == 0) && ride == nullptr)) return LGCN_OK;
+    if (N == 0 || (n_items == 0 && n_splits == 0)) return LGCN_OK;
     SpmmArgs a{items, n_items, splits, n_splits, col, val, x_lo, x_hi, x_split, e_lo, e_hi, e_split,
                y, acc_lo, acc_hi, acc_split, partial, d, mode, div, mul, run, chunks};
-    a.ride = ride;
     return dispatch(a, N, as_stream(stream), pass, run, nullptr);
 }
 
@@ -988,10 +945,6 @@ int lgcn_spmm_run_slices(const lgcn_item_t* items, const int64_t* slice_offsets,
 }
 int lgcn_spmm_blocksplit(LGCN_SPMM_PARAMS, const lgcn_item_t* chunks) {
     return spmm_impl(LGCN_SPMM_ARGS, PASS_BSPLIT, nullptr, chunks);
-}
-
-int lgcn_spmm_blocksplit_ride(LGCN_SPMM_PARAMS, const lgcn_item_t* chunks, const lgcn_adam_ride_t* ride) {
-    return spmm_impl(LGCN_SPMM_ARGS, PASS_BSPLIT, nullptr, chunks, ride);
 }
 
 // lgcn_pass_t -> SpmmArgs, validated as a plain pass of width d over N rows.

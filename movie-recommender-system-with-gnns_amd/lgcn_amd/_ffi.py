@@ -74,10 +74,6 @@ _SIGS = {
     "lgcn_spmm_blocksplit": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
                               _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp],
                              ctypes.c_int),
-    "lgcn_spmm_blocksplit_ride": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32,
-                                   _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _vp, _vp,
-                                   _vp],
-                                  ctypes.c_int),
     "lgcn_spmm_pair": ([_vp, _vp, _i64, _i32, _i32, _vp], ctypes.c_int),
     "lgcn_spmm_pass": ([_vp, _i64, _i32, _i32, _vp], ctypes.c_int),
     "lgcn_stack_mean_rows": ([_vp, _vp, _i32, _i64, _i32, _vp, _f32, _f32, _vp], ctypes.c_int),
@@ -158,16 +154,6 @@ class Pass(ctypes.Structure):
     def __init__(self, *args, n_split_big: int = -1, **kw):
         super().__init__(*args, **kw)
         self.n_split_big = n_split_big
-
-
-class AdamRide(ctypes.Structure):
-    """lgcn_adam_ride_t (include/lgcn.h, ABI 7): the Adam catch-up riding in a block-split launch."""
-    _fields_ = [("rows", ctypes.c_void_p), ("n_rows", ctypes.c_int64), ("skip", ctypes.c_void_p),
-                ("p_lo", ctypes.c_void_p), ("p_hi", ctypes.c_void_p), ("m_lo", ctypes.c_void_p),
-                ("m_hi", ctypes.c_void_p), ("v_lo", ctypes.c_void_p), ("v_hi", ctypes.c_void_p),
-                ("split", ctypes.c_int64), ("last", ctypes.c_void_p), ("step", ctypes.c_void_p),
-                ("consts", ctypes.c_void_p), ("one_minus_beta1", ctypes.c_float), ("beta2", ctypes.c_float),
-                ("eps", ctypes.c_float), ("max_replays", ctypes.c_int32)]
 
 
 class Tuning(ctypes.Structure):

@@ -16,6 +16,7 @@ the union of the ranks' rows.
 """
 from __future__ import annotations
 
+
 import torch
 import torch.distributed as dist
 

@@ -182,12 +182,10 @@ def bipartite(ei: torch.Tensor, U: int) -> bool:
 def train_epoch(model, optimizer, batches, device):
     """Run the fused step over the batches iterator until it ends or yields a batch the fused step
     cannot take (not a bipartite user-item edge list). Returns (sum over the fused batches of
-    loss * edges as a device tensor or None, their total edges, the batches read but not taken
-    (a list, empty when the epoch ran fused to its end), fused steps run). The torch optimizer
-    holds the row-lazy Adam's state whenever this returns, so the caller runs the reference loop
-    over the returned batches and then the rest of the iterator (it is read once, one batch
-    ahead: one-shot loaders lose no batch). The batch read ahead is the step's next_batch: its
-    users' Adam catch-up rides in the current step's launches (FusedTrainStep._ride)."""
+    loss * edges as a device tensor or None, their total edges, the first batch not taken or None,
+    fused steps run). The torch optimizer holds the row-lazy Adam's state whenever this returns,
+    so the caller runs the reference loop from the returned batch on (the iterator is read once:
+    one-shot loaders lose no batch)."""
     fast = _FAST.get(optimizer)
     if fast is None or fast.model is not model:
         fast = _Fast(model, optimizer)
@@ -198,34 +196,23 @@ def train_epoch(model, optimizer, batches, device):
         n = None
     fast.load_state(optimizer)
     fast.size_for(n)
-    total, total_w, steps, leftover = None, 0, 0, []
+    total, total_w, steps, leftover = None, 0, 0, None
     U = model.num_users
-    it = iter(batches)
-
-    def take():
-        b = next(it, None)
-        if b is None:
-            return None, None
-        e = fast.device_edge_index(b.edge_index, device)
-        return b, (e if fast.eligible(e, U) else None)
-
     try:
-        batch, ei = take()
-        while batch is not None:
-            if ei is None:
-                leftover = [batch]
+        for batch in batches:
+            ei = fast.device_edge_index(batch.edge_index, device)
+            if not fast.eligible(ei, U):
+                leftover = batch
                 break
-            nxt, nxt_ei = take()
             if fast.opt.steps + 1 > fast.opt.max_steps:  # a loader without len(): grow mid-epoch
                 fast.step.sync()  # every row current before the constants are regenerated
                 fast.reserve(fast.opt.steps + 1)
-            loss = fast.step.step(_Batch(ei), _Batch(nxt_ei) if nxt_ei is not None else None)
+            loss = fast.step.step(_Batch(ei))
             steps += 1
             w = int(ei.shape[1])
             total_w += w
             contrib = loss.detach().double() * w
             total = contrib if total is None else total + contrib
-            batch, ei = nxt, nxt_ei
     finally:
         if steps:
             fast.store_state(optimizer)

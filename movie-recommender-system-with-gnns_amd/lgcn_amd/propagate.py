@@ -11,7 +11,6 @@ No intermediate x_k is saved: Â is linear, so the backward needs only the plan 
 """
 from __future__ import annotations
 
-import ctypes
 
 import numpy as np
 import torch
@@ -35,12 +34,10 @@ def _f32(x: float) -> float:
 
 
 def spmm(direction, N: int, d: int, x, e, acc, y, mode: int, div: float = 1.0, mul: float = 1.0,
-         partial: torch.Tensor | None = None, stream: int | None = None, ride=None) -> None:
+         partial: torch.Tensor | None = None, stream: int | None = None) -> None:
     """One layer: one lgcn_spmm call over a CsrDirection, or the per-slice lgcn_spmm_run launches
     (+ hub combine) over a SlicedDirection. x / e / acc are split tables: (lo, hi, split) with
-    hi=None for a single [N, d] table (split = N). ride: an _ffi.AdamRide that rides in the
-    launch when it is a block-split one (the Cluster-GCN batch plans; lgcn_spmm_blocksplit_ride),
-    ignored otherwise."""
+    hi=None for a single [N, d] table (split = N)."""
     lib = _ffi.load()
     if stream is None:
         stream = _ffi.stream_of(acc[0].device)
@@ -68,9 +65,6 @@ def spmm(direction, N: int, d: int, x, e, acc, y, mode: int, div: float = 1.0, m
                 direction.col.data_ptr(), direction.val.data_ptr(), N, d,
                 _ffi.ptr(xl), _ffi.ptr(xh), xs, _ffi.ptr(el), _ffi.ptr(eh), es,
                 _ffi.ptr(y), _ffi.ptr(al), _ffi.ptr(ah), as_, None, mode, div, mul, stream, chunks.data_ptr())
-        if ride is not None:
-            _ffi.check(lib.lgcn_spmm_blocksplit_ride(*args, ctypes.byref(ride)), "lgcn_spmm_blocksplit_ride")
-            return
         if _launch_timer is not None:
             with _launch_timer(d, 1):
                 rc = lib.lgcn_spmm_blocksplit(*args)
@@ -111,10 +105,8 @@ def _check_tables(user_w: torch.Tensor, item_w: torch.Tensor, plan: PropagationP
     return U, I, d
 
 
-def propagate_forward(user_w: torch.Tensor, item_w: torch.Tensor, plan: PropagationPlan, K: int,
-                      ride=None) -> torch.Tensor:
-    """out[N, d] = LightGCN final embedding (users first, then items). ride: an _ffi.AdamRide
-    carried by each layer's launch when the plan's schedule is block-split (train_step)."""
+def propagate_forward(user_w: torch.Tensor, item_w: torch.Tensor, plan: PropagationPlan, K: int) -> torch.Tensor:
+    """out[N, d] = LightGCN final embedding (users first, then items)."""
     U, I, d = _check_tables(user_w, item_w, plan)
     N = U + I
     dev = user_w.device
@@ -139,16 +131,16 @@ def propagate_forward(user_w: torch.Tensor, item_w: torch.Tensor, plan: Propagat
             return out
     partial = torch.empty((f.n_partials, d), dtype=torch.float32, device=dev) if f.n_partials else None
     if K == 1:
-        spmm(f, N, d, x0, x0, acc, None, _ffi.EPI_FINAL_E, div, mul, partial, stream, ride=ride)
+        spmm(f, N, d, x0, x0, acc, None, _ffi.EPI_FINAL_E, div, mul, partial, stream)
         return out
     bufs = [torch.empty((N, d), dtype=torch.float32, device=dev) for _ in range(min(2, K - 1))]
-    spmm(f, N, d, x0, x0, acc, bufs[0], _ffi.EPI_INIT, 1.0, 1.0, partial, stream, ride=ride)
+    spmm(f, N, d, x0, x0, acc, bufs[0], _ffi.EPI_INIT, 1.0, 1.0, partial, stream)
     for k in range(2, K):
         src = bufs[(k - 2) % len(bufs)]
         dst = bufs[(k - 1) % len(bufs)]
-        spmm(f, N, d, (src, None, N), None, acc, dst, _ffi.EPI_ADD, 1.0, 1.0, partial, stream, ride=ride)
+        spmm(f, N, d, (src, None, N), None, acc, dst, _ffi.EPI_ADD, 1.0, 1.0, partial, stream)
     last = bufs[(K - 2) % len(bufs)]
-    spmm(f, N, d, (last, None, N), None, acc, None, _ffi.EPI_FINAL_ACC, div, mul, partial, stream, ride=ride)
+    spmm(f, N, d, (last, None, N), None, acc, None, _ffi.EPI_FINAL_ACC, div, mul, partial, stream)
     return out
 
 
@@ -163,6 +155,8 @@ def _forward_sliced_ride(f, N: int, U: int, d: int, x0, acc, K: int, div: float,
     that the previous layer's split rows are being read from). The last group's split rows get a
     combine launch of their own. Each row: the slice launches and combine of propagate_forward,
     in the same order — bitwise its result."""
+    import ctypes
+
     lib = _ffi.load()
     dev = acc[0].device
     r = f._ride
@@ -212,6 +206,8 @@ def _forward_sliced_ride(f, N: int, U: int, d: int, x0, acc, K: int, div: float,
 def _ride_layers(f, N, d, K, r, groups, writes, layer, ride_pass, scratch, acc, offs, stream, lib):
     """The K layers' slice-group launches of _forward_sliced_ride; returns the last group's pending
     split rows (combined by the caller's final launch)."""
+    import ctypes
+
     al, ah, as_ = acc
     pending = None
     for k in range(1, K + 1):
@@ -270,8 +266,7 @@ def propagate_backward(dout: torch.Tensor, plan: PropagationPlan, U: int, K: int
     return grad_user, grad_item
 
 
-def propagate_backward_seeded(grad_user: torch.Tensor, grad_item: torch.Tensor, plan: PropagationPlan, K: int,
-                              ride=None) -> None:
+def propagate_backward_seeded(grad_user: torch.Tensor, grad_item: torch.Tensor, plan: PropagationPlan, K: int) -> None:
     """In-place backward for the sparse batch step: on entry the two gradient tables hold the seed
     g = (dF * mul) / div for EVERY row; on exit they hold dL/dx0. Only the plan's scheduled rows
     change (with a touched-only plan, rows no batch edge reaches keep g, which is their exact
@@ -289,14 +284,14 @@ def propagate_backward_seeded(grad_user: torch.Tensor, grad_item: torch.Tensor, 
     if K == 1:
         # the gather source must not alias the table being written
         src = torch.cat([grad_user, grad_item])
-        spmm(b, N, d, (src, None, N), g, g, None, _ffi.EPI_INIT, 1.0, 1.0, partial, stream, ride=ride)
+        spmm(b, N, d, (src, None, N), g, g, None, _ffi.EPI_INIT, 1.0, 1.0, partial, stream)
         return
     bufs = [torch.empty((N, d), dtype=torch.float32, device=dev) for _ in range(min(2, K - 1))]
     cur = g
     for step in range(K):
         last = step == K - 1
         acc = g if last else (bufs[step % len(bufs)], None, N)
-        spmm(b, N, d, cur, g, acc, None, _ffi.EPI_INIT, 1.0, 1.0, partial, stream, ride=ride)
+        spmm(b, N, d, cur, g, acc, None, _ffi.EPI_INIT, 1.0, 1.0, partial, stream)
         cur = acc
 
 

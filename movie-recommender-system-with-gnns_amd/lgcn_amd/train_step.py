@@ -173,8 +173,6 @@ class _BatchState:
             self.fixed_dense, self.fixed_sparse, self.fixed_touched = segment_directions(
                 self.keys[:2 * B], N, chunk=32, row_mask=self.plan.touched)
             self.touched_rows = torch.nonzero(self.plan.touched).squeeze(1).to(torch.int32).contiguous()
-            # the batch's user rows: what the previous step's riding catch-up advances (train_step._ride)
-            self.touched_users = self.touched_rows[self.touched_rows < U].contiguous()
         elif self.small:
             self.fixed_dense, self.fixed_sparse = segment_directions(self.keys[:2 * B], N, chunk=32)
         if self.small and B >= sorted_scatter_min_b():
@@ -382,7 +380,7 @@ class FusedTrainStep:
         """Forget every batch's captured hipGraph (the next step of each batch recaptures it):
         needed when a buffer a graph reads moved, e.g. RowLazyAdam.reserve() grew its constants."""
         for st in self._states.values():
-            for a in ("graph", "graph_post", "graph_loss", "graph_grads", "graph_ride"):
+            for a in ("graph", "graph_post", "graph_loss", "graph_grads"):
                 if hasattr(st, a):
                     setattr(st, a, None)
 
@@ -499,44 +497,17 @@ class FusedTrainStep:
                                      st.loss_part.data_ptr(), stream), "lgcn_bpr_loss")
         return c.reg_coeff(self.coeff)
 
-    def _ride(self, st: _BatchState, nxt: _BatchState | None):
-        """The riding Adam catch-up (lgcn_adam_ride_t) of step `st` for the batch after it: nxt's
-        user rows, skipping st's touched rows, advanced by at most tuning.adam_ride_replays
-        zero-gradient steps in each of st's block-split launches (2K of them), up to the step in
-        progress. Correct whichever batch really comes next: a user row outside st's touched set
-        has a zero gradient in this step (negatives are items), and the replays are the catch-up's
-        arithmetic — so a captured graph may keep the rows it was captured with. None when there is
-        nothing to ride (no next batch, an exchange: the union's rows are known only after it)."""
-        from . import tuning
-
-        R = tuning.get().adam_ride_replays
-        if (nxt is None or R <= 0 or not self.lazy or self.exchange is not None or not st.lazy or not nxt.lazy
-                or nxt is st or nxt.touched_users.numel() == 0):
-            return None
-        key = (id(nxt), R, self.optimizer.consts.data_ptr())
-        cached = getattr(st, "_ride_cache", None)
-        if cached is not None and cached[0] == key:
-            return cached[1]
-        opt, m = self.optimizer, self.model
-        rows = nxt.touched_users  # kept alive by the cache below while a graph may replay it
-        rec = _ffi.AdamRide(rows.data_ptr(), rows.numel(), st.plan.touched.data_ptr(), opt.uw.data_ptr(),
-                            opt.iw.data_ptr(), opt.m[0].data_ptr(), opt.m[1].data_ptr(), opt.v[0].data_ptr(),
-                            opt.v[1].data_ptr(), m.num_users, opt.last.data_ptr(), opt.step_dev.data_ptr(),
-                            opt.consts.data_ptr(), 1 - opt.betas[0], opt.betas[1], opt.eps, R)
-        st._ride_cache = (key, rec, rows)
-        return rec
-
-    def _step_lazy(self, st: _BatchState, draw: bool = True, ride=None) -> torch.Tensor:
+    def _step_lazy(self, st: _BatchState, draw: bool = True) -> torch.Tensor:
         """The whole batch step with the row-lazy optimizer: catch the batch's rows (touched rows
         and this step's negatives) up, forward, loss, gradient rows written only where the step
         can make them nonzero, backward, [row exchange], clip + Adam on exactly those rows."""
-        loss = self._lazy_grads(st, draw, ride)
+        loss = self._lazy_grads(st, draw)
         if self.exchange is not None:
             self.exchange.gather()
         self._lazy_update(st)
         return loss
 
-    def _lazy_grads(self, st: _BatchState, draw: bool = True, ride=None) -> torch.Tensor:
+    def _lazy_grads(self, st: _BatchState, draw: bool = True) -> torch.Tensor:
         m = self.model
         opt = self.optimizer
         lib = _ffi.load()
@@ -554,7 +525,7 @@ class FusedTrainStep:
                 self._draw(st)
             if not self.owner:  # owner-sharded: the rows were fetched current by the previous step
                 opt.catch_up(st.touched_rows, st.neg, U)
-            out = propagate_forward(uw.detach(), iw.detach(), st.plan, K, ride=ride)
+            out = propagate_forward(uw.detach(), iw.detach(), st.plan, K)
             reg_coeff = self._bpr(lib, st, out, uw, iw, U, N, B, d, div, mul, stream)
             gu, gi = opt.gu, opt.gi
             grads = (gu, gi, U)
@@ -564,7 +535,7 @@ class FusedTrainStep:
             # ... the negatives' rows added (stored where the row is outside the touched set)
             scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream, uw, iw, reg_coeff,
                               (st.terms, d, self.coeff, st.loss) if loss_fused(st, I, self.cols) else None)
-            propagate_backward_seeded(gu, gi, st.plan, K, ride=ride)
+            propagate_backward_seeded(gu, gi, st.plan, K)
             add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, reg_coeff, stream)
             add_negative_reg_rows(lib, st, gu, gi, U, d, uw, iw, reg_coeff, stream)
             ex = self.exchange
@@ -752,31 +723,27 @@ class FusedTrainStep:
         allreduce_grads([self.model.user_embedding.weight, self.model.item_embedding.weight], self.world)
 
     def step(self, batch, next_batch=None) -> torch.Tensor:
-        """One training step on batch. next_batch: the batch the NEXT step will take — owner-sharded:
-        its rows are fetched from their owners at the end of this step; row-lazy without an
-        exchange: its user rows' Adam catch-up rides in this step's block-split launches (_ride)."""
+        """One training step on batch. next_batch (owner-sharded: the batch the NEXT step will
+        take): its rows are fetched from their owners at the end of this step."""
         if self.owner:
             st = self.state(batch.edge_index)
             nxt = self.state(next_batch.edge_index) if next_batch is not None else None
             if not st.lazy or (nxt is not None and not nxt.lazy):
                 raise ValueError("lazy step needs a batch whose 3B contribution ids fit int32 (3B < 2^31)")
             return self._step_owner(st, nxt)
-        loss = self._step_replicated(batch, next_batch)
+        loss = self._step_replicated(batch)
         self._k += 1
         return loss
 
-    def _step_replicated(self, batch, next_batch=None) -> torch.Tensor:
+    def _step_replicated(self, batch) -> torch.Tensor:
         if self.lazy:
             st = self.state(batch.edge_index)
             if not st.lazy:
                 raise ValueError("lazy step needs a batch whose 3B contribution ids fit int32 (3B < 2^31)")
-            ride = None
-            if next_batch is not None and self.exchange is None:
-                ride = self._ride(st, self.state(next_batch.edge_index))
             if not self.graphs:
-                return self._step_lazy(st, ride=ride)
+                return self._step_lazy(st)
             if getattr(st, "graph", None) is None:
-                loss = self._step_lazy(st, ride=ride)  # real first step (warms allocations), then capture
+                loss = self._step_lazy(st)  # real first step (warms allocations), then capture
                 torch.cuda.synchronize()
                 steps = self.optimizer.steps
                 g = torch.cuda.CUDAGraph()
@@ -785,12 +752,12 @@ class FusedTrainStep:
                     g = _SegmentedGraph()
                     self.cols.capture = g
                     try:
-                        st.graph_loss = g.capture(lambda: self._step_lazy(st, draw=False, ride=ride))
+                        st.graph_loss = g.capture(lambda: self._step_lazy(st, draw=False))
                     finally:
                         self.cols.capture = None
                 elif self.exchange is None:
                     with torch.cuda.graph(g):
-                        st.graph_loss = self._step_lazy(st, draw=False, ride=ride)
+                        st.graph_loss = self._step_lazy(st, draw=False)
                 else:  # two halves: the all_gather between them runs eagerly
                     with torch.cuda.graph(g):
                         st.graph_loss = self._lazy_grads(st, draw=False)
@@ -799,9 +766,6 @@ class FusedTrainStep:
                         self._lazy_update(st)
                 self.optimizer.steps = steps  # the capture ran no step
                 st.graph = g
-                # the captured launches read the ride's row list: kept alive with the graph (a later
-                # step of this batch may name another next batch; the graph keeps these rows)
-                st.graph_ride = st._ride_cache if ride is not None else None
                 return loss
             if self.optimizer.steps + 1 > self.optimizer.max_steps:
                 raise RuntimeError("RowLazyAdam: max_steps exceeded")

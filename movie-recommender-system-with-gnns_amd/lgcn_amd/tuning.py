@@ -45,9 +45,6 @@ class Tuning:
     harness_fused: bool = True
     # run the exchanges' RCCL branches even on a gloo group (tests: gloo carries the bytes)
     device_collectives: bool = False
-    # row-lazy Adam: zero-gradient replays per row that the next batch's user catch-up may run in
-    # each block-split launch of the current step (lgcn_adam_ride_t; 0 = no riding catch-up)
-    adam_ride_replays: int = 8
     # --- native (lgcn_tuning_t) -----------------------------------------------------------------
     spmm_tail: int = -1
     spmm_index_rounds: int = 0
@@ -63,8 +60,6 @@ class Tuning:
             raise ValueError(f"neg_grouping must be 'count' or 'radix', got {self.neg_grouping!r}")
         if self.sorted_scatter_min_b < 1 or self.recall_subset < 1:
             raise ValueError("sorted_scatter_min_b and recall_subset must be >= 1")
-        if self.adam_ride_replays < 0:
-            raise ValueError("adam_ride_replays must be >= 0")
 
 
 _current = Tuning()

@@ -96,7 +96,7 @@ def train(model: torch.nn.Module, optimizer: torch.optim.Optimizer, train_loader
     why = "model not on a ROCm device"
     total_loss, total_w = None, 0
     batches = train_loader
-    rest = []  # batches the fused step read but did not take: the reference loop's first
+    rest = None  # the first batch the reference loop takes after fused steps
     weight = getattr(getattr(model, "user_embedding", None), "weight", None)
     if weight is not None and weight.is_cuda:
         from lgcn_amd import harness
@@ -107,7 +107,7 @@ def train(model: torch.nn.Module, optimizer: torch.optim.Optimizer, train_loader
             if hasattr(train_loader, "__len__"):
                 batches = _Sized(batches, len(train_loader))
             total_loss, total_w, rest, steps = harness.train_epoch(model, optimizer, batches, device)
-            if not rest:
+            if rest is None:
                 LAST_TRAIN_PATH = "fused"
                 if total_loss is None:
                     raise ZeroDivisionError("empty train loader")
@@ -116,7 +116,7 @@ def train(model: torch.nn.Module, optimizer: torch.optim.Optimizer, train_loader
             if steps:
                 why = f"fused for {steps} batch(es), then reference from a batch that is not a bipartite user-item edge list"
     LAST_TRAIN_PATH = f"reference: {why}"
-    for batch in (_chain(rest, batches) if rest else batches):
+    for batch in (_chain(rest, batches) if rest is not None else batches):
         contrib, w = _reference_step(model, optimizer, batch, device)
         total_w += w
         total_loss = contrib if total_loss is None else total_loss + contrib
@@ -139,7 +139,7 @@ class _Sized:
 
 
 def _chain(first, rest):
-    yield from first
+    yield first
     yield from rest
 
 
