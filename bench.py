@@ -489,13 +489,15 @@ def main():
     ap.add_argument("--no-graphs", action="store_true", help="train: run the fused step eagerly (no hipGraph replay)")
     ap.add_argument("--exchange", action="store_true",
                     help="train, N=1: run the row exchange anyway (measures its kernels; N>1 always uses it)")
-    ap.add_argument("--dp-mode", choices=["replicated", "owner", "columns"], default="columns",
-                    help="train, N > 1: column-sharded exact training (the default: every rank the same batches "
-                         "on d/N columns, one [B, 6] all_reduce per step — the one-GPU step's semantics, so "
-                         "Recall is the one-GPU run's), or data parallel over disjoint parts with a replicated "
-                         "row-lazy Adam (all_gather of every rank's gradient rows) or an owner-sharded one (two "
+    ap.add_argument("--dp-mode", choices=["auto", "replicated", "owner", "columns"], default="auto",
+                    help="train, N > 1: column-sharded exact training (every rank the same batches on d/N "
+                         "columns, one [B, 6] all_reduce per step — the one-GPU step's semantics, so Recall is "
+                         "the one-GPU run's), or data parallel over disjoint parts with a replicated row-lazy "
+                         "Adam (all_gather of every rank's gradient rows) or an owner-sharded one (two "
                          "all_to_alls) — W-times fewer, larger Adam steps: Recall@20 within the +-0.002 band "
-                         "with little margin at W = 8, Recall@100 outside it (tests/test_gpu_dp_recall.py)")
+                         "with little margin at W = 8, Recall@100 outside it (tests/test_gpu_dp_recall.py). "
+                         "auto: the projection's pick (tools/project_c4.py, DESIGN §7): columns at N <= 2, "
+                         "owner from N = 4")
     ap.add_argument("--no-harness", action="store_true",
                     help="train, N=1: skip timing utils.train_test.train() both ways after the bench line's run")
     ap.add_argument("--dense-adam", action="store_true",
@@ -971,6 +973,11 @@ def run_train(args):
     model = LightGCN(U, I, num_layers=K, dim_h=d).to(dev)
     lazy = not (args.autograd or args.torch_adam or args.dense_adam)
     dp_mode = args.dp_mode if world > 1 else "replicated"
+    if dp_mode == "auto":
+        # tools/project_c4.py on the C3 batches (profiles/r05g_c4proj/): at W = 2 no mode beats one GPU
+        # by much and columns keeps the one-GPU semantics; from W = 4 the owner-sharded exchange is
+        # the fastest (W = 8: 1.9x at 100 GB/s, 2.7x at 200, against ~1.0x for columns)
+        dp_mode = "columns" if world <= 2 else "owner"
     if dp_mode != "replicated" and not lazy:
         raise SystemExit("--dp-mode owner / columns need the row-lazy Adam (no --autograd/--torch-adam/--dense-adam)")
     cols = None

@@ -8,8 +8,10 @@ star: Recall@20 within +-0.002 of the reference), at BASELINE configs[0]'s size
   fewer, larger steps than the reference's one-part-per-step loop (reference
   utils/train_test.py:86-101 over data/dataset_handler.py:285). Recall@20 is held to the north
   star's +-0.002 (measured 0.0015-0.0018 in round 3: inside, with little margin); Recall@100 is
-  printed with its band status (0.0030-0.0032 in round 3: outside). That is why bench.py's
-  default --dp-mode for training on several GPUs is "columns", not this mode.
+  printed with its band status (0.0030-0.0032 in round 3: outside). bench.py's default --dp-mode
+  ("auto") keeps "columns" at 2 ranks and takes the owner-sharded form of this mode from 4 ranks,
+  where it is the only one projected to scale (tools/project_c4.py): the north star's
+  Recall@20 holds for it, its Recall@100 does not.
 * Column-sharded (lgcn_amd.train_step.ColumnGroup, SURVEY §8e's parity-preserving alternative):
   every rank steps the reference's schedule on d / W columns; one all_reduce of the triplets'
   [B, 6] dot products and norms and one all_gather of the clip norm's partials per step. Its
