@@ -260,7 +260,12 @@ def test_plan_cache_reuse_and_invalidation(gpu):
     et = torch.from_numpy(ei).to(gpu)
     p1 = model.plan_for(et)
     assert model.plan_for(et) is p1
-    et[0, 0] = et[0, 0]  # in-place write bumps the version counter
+    # plans are found by content (lgcn_amd._cache): a new tensor of the same edges — what the
+    # reference's PyG loader collates every epoch — gets the same plan
+    assert model.plan_for(et.clone()) is p1
+    et[0, 0] = et[0, 0]  # in-place write bumps the version counter: re-keyed, the same edges
+    assert model.plan_for(et) is p1
+    et[:, [0, 1]] = et[:, [1, 0]].clone()  # an in-place change of the edge list: a new plan
     assert model.plan_for(et) is not p1
 
 
