@@ -475,7 +475,8 @@ def main():
     ap.add_argument("--shard", default=None,
                     help="c2, N > 1: RxF grid (R row groups x F column groups, R*F = N); default: every "
                          "lgcn_amd.sharded.grid_candidates grid is timed for a few steps and the fastest runs")
-    ap.add_argument("--exchange-mode", choices=["allgather", "p2p", "reduce", "reduce-fused"], default="allgather",
+    ap.add_argument("--exchange-mode", choices=["allgather", "p2p", "reduce", "reduce-fused", "reduce-a2a",
+                                                "reduce-a2a-fused"], default="allgather",
                     help="c2 with --shard and R > 1: one all_gather per block, or sends to every peer")
     ap.add_argument("--workload", choices=["propagate", "train"], default="propagate",
                     help="propagate: C2 headline (default); train: C3/C4 Cluster-GCN training steps")
@@ -591,14 +592,15 @@ def main():
                             mode=None, step=lambda: lgcn_amd.propagate_forward(uw_c, iw_c, cplan, K))
             if (grid.R, grid.F) not in groups:  # collective: every rank creates the column groups
                 groups[(grid.R, grid.F)] = grid.exchange_group(dist)
-            if mode in ("reduce", "reduce-fused"):
+            if str(mode).startswith("reduce"):
                 # users sharded, item rows all-reduced per layer (lgcn_amd.sharded.ReducePlan);
-                # reduce-fused: a layer's two passes as one lgcn_spmm_pair launch (+ one combine)
+                # *-fused: a layer's two passes as one lgcn_spmm_pair launch (+ one combine);
+                # reduce-a2a*: the all_reduce as all_to_all + ordered slice sums + all_gather
                 ushards = UserShards.build(in_deg, U, grid.R)
                 rplan = ReducePlan(ei, ushards, grid.row_group, c1 - c0, chunk)
-                red = ItemReducer(grid.R, groups[(grid.R, grid.F)])
+                red = ItemReducer(grid.R, groups[(grid.R, grid.F)], method="a2a" if "a2a" in mode else "ring")
                 x0u, x0i = user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous()
-                fused = mode == "reduce-fused"
+                fused = mode.endswith("fused")
                 return dict(grid=grid, shards=ushards, splan=rplan, scheds=[rplan.users, rplan.partial], ex=red,
                             mode=mode, step=lambda: propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused))
             shards = RowShards.build(in_deg, U, grid.R)

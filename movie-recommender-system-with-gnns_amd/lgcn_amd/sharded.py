@@ -187,8 +187,9 @@ def grid_candidates(world: int, d: int, bipartite: bool = True,
             out.append((R, F, None))
         else:
             out += [(R, F, m) for m in (EXCHANGE_MODES if R >= 3 else EXCHANGE_MODES[:1])]
-            if bipartite:  # users sharded, item rows all-reduced (ReducePlan), overlapped or fused order
-                out += [(R, F, "reduce"), (R, F, "reduce-fused")]
+            if bipartite:  # users sharded, item rows all-reduced (ReducePlan), overlapped or fused order,
+                # by RCCL's all_reduce or by all_to_all + ordered sums + all_gather (ItemReducer "a2a")
+                out += [(R, F, "reduce"), (R, F, "reduce-fused"), (R, F, "reduce-a2a"), (R, F, "reduce-a2a-fused")]
     if any(F > 1 for _, F, _ in out) and world < 4:
         out = [c for c in out if c[1] > 1]
     # the peer-send candidates last: batch_isend_irecv is the one exchange outside RCCL's plain
@@ -656,15 +657,69 @@ class ReducePlan:
 class ItemReducer:
     """Sum of the R item-partial tables of a column group: one all_reduce per layer (nccl: RCCL on
     a side stream after an event on the compute stream, waited on before the rows are read; gloo:
-    synchronous, through host memory)."""
+    synchronous, through host memory).
 
-    def __init__(self, R: int, group=None):
+    method "a2a" (round 5) replaces RCCL's all_reduce by its two halves written out: one
+    all_to_all_single sends slice s of the rank's partial table to group rank s (on a fully
+    connected xGMI mesh every pair has its own link, so the R - 1 transfers run at once instead of
+    around a ring), the owner sums the R slices it received in rank order (lgcn_stack_mean_rows with
+    div = mul = 1: ((p_0 + p_1) + ...) exactly), and one all_gather_into_tensor returns the reduced
+    slices to every rank; the last layer stops after the sum (its reduce_scatter). Same bytes as a
+    ring all_reduce, other latency and link use: bench.py times both (reduce-a2a candidates)."""
+
+    def __init__(self, R: int, group=None, method: str = "ring"):
         import torch.distributed as dist
 
-        self.dist, self.R, self.group = dist, int(R), group
+        if method not in ("ring", "a2a"):
+            raise ValueError(f"ItemReducer method {method!r}: 'ring' or 'a2a'")
+        self.dist, self.R, self.group, self.method = dist, int(R), group, method
         self.nccl = R > 1 and device_collectives(group)
         self.stream = None
+        self.ws = {}
         self.bytes = 0  # ring all_reduce traffic received per rank over the run
+
+    def _a2a(self, buf: torch.Tensor, out_share: torch.Tensor | None, rank: int):
+        """The a2a method's reduce: rank `rank` of the group sums slice `rank` of the R partial
+        tables in rank order into out_share (or, None, a workspace all-gathered back into buf)."""
+        R, dist = self.R, self.dist
+        per = buf.shape[0] // R
+        if not self.nccl:  # gloo through host memory: the same slices, sums and order
+            host = buf.cpu()
+            recv = torch.empty_like(host)
+            dist.all_to_all_single(recv, host, group=self.group)
+            acc = recv[:per].clone()
+            for s in range(1, R):
+                acc += recv[s * per:(s + 1) * per]
+            if out_share is not None:
+                out_share.copy_(acc)
+                return None
+            parts = [torch.empty_like(acc) for _ in range(R)]
+            dist.all_gather(parts, acc, group=self.group)
+            buf.copy_(torch.cat(parts))
+            return None
+        import ctypes
+
+        key = (tuple(buf.shape), buf.device)
+        if key not in self.ws:
+            self.ws[key] = (torch.empty_like(buf), torch.empty((per, buf.shape[1]), dtype=buf.dtype, device=buf.device))
+        recv, mine = self.ws[key]
+        dst = out_share if out_share is not None else mine
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(buf.device)
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(buf.device))
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(ready)
+            dist.all_to_all_single(recv, buf, group=self.group)
+            ys = (ctypes.c_void_p * (R - 1))(*[recv[s * per:(s + 1) * per].data_ptr() for s in range(1, R)])
+            _ffi.check(_ffi.load().lgcn_stack_mean_rows(recv[:per].data_ptr(), ys, R - 1, per, buf.shape[1],
+                                                        dst.data_ptr(), 1.0, 1.0, _ffi.stream_of(buf.device)),
+                       "lgcn_stack_mean_rows (a2a slice sum)")
+            if out_share is None:
+                dist.all_gather_into_tensor(buf, mine, group=self.group)
+            done = torch.cuda.Event()
+            done.record(self.stream)
+        return done
 
     def start_scatter(self, buf: torch.Tensor, out: torch.Tensor, rank: int):
         """out = this group member's 1/R row share of the sum of buf over the group (buf's rows a
@@ -673,6 +728,8 @@ class ItemReducer:
         if self.R == 1:
             out.copy_(buf)
             return None
+        if self.method == "a2a":
+            return self._a2a(buf, out, rank)
         if self.nccl:
             if self.stream is None:
                 self.stream = torch.cuda.Stream(buf.device)
@@ -694,6 +751,8 @@ class ItemReducer:
         self.bytes += int(2 * (self.R - 1) / self.R * buf.numel() * buf.element_size())
         if self.R == 1:
             return None
+        if self.method == "a2a":
+            return self._a2a(buf, None, self.dist.get_rank(self.group))
         if self.nccl:
             if self.stream is None:
                 self.stream = torch.cuda.Stream(buf.device)

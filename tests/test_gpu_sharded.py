@@ -182,7 +182,7 @@ def _check_sharded_ranks(gpu, tune, tmp_path, case, world, F, mode, dc):
     assert sum(int(m[0]) for m in meta) == n_hubs
 
 
-def _reduce_worker(rank, world, port, case, out_dir, F=1, dc=False, fused=False):
+def _reduce_worker(rank, world, port, case, out_dir, F=1, dc=False, fused=False, method="ring"):
     import sys
 
     from conftest import PKG, ROOT
@@ -209,7 +209,7 @@ def _reduce_worker(rank, world, port, case, out_dir, F=1, dc=False, fused=False)
     c0, c1 = grid.cols
     shards = UserShards.build(np.bincount(ei[1], minlength=U + I), U, grid.R)
     rplan = ReducePlan(torch.from_numpy(ei).to(dev), shards, grid.row_group, c1 - c0, chunk)
-    red = ItemReducer(grid.R, grid.exchange_group(dist))
+    red = ItemReducer(grid.R, grid.exchange_group(dist), method=method)
     ou, oi = propagate_forward_reduced(torch.from_numpy(uw[:, c0:c1].copy()).to(dev),
                                        torch.from_numpy(iw[:, c0:c1].copy()).to(dev), rplan, K, red, fused=fused)
     ua, ub = shards.users(grid.row_group)
@@ -252,7 +252,25 @@ def test_reduce_mode_fused_pairs(gpu, tmp_path, case, world, F):
         assert np.array_equal(np.load(fused_dir / f), np.load(plain_dir / f)), f
 
 
-def _check_reduce_ranks(gpu, tmp_path, case, world, F, dc, fused=False):
+@pytest.mark.parametrize("case,world,F,fused", [("ml25m5_plain", 4, 2, False), ("ml25m5_sliced", 8, 2, False),
+                                                ("hub_sliced", 3, 1, True), ("sub_K2_d128", 2, 1, False)])
+def test_reduce_mode_a2a_device_collectives_bitwise_host_path(gpu, tmp_path, case, world, F, fused):
+    """ItemReducer method "a2a" (all_to_all_single of the partial tables' slices, the owner's
+    slice sum in rank order by lgcn_stack_mean_rows, all_gather_into_tensor; the last layer stops
+    after the sum): the RCCL branch's code (device collectives on a side stream, gloo carrying the
+    bytes) within 1e-5 of the oracle and bitwise the same algorithm through host memory."""
+    dev_dir, host_dir = tmp_path / "dc", tmp_path / "host"
+    dev_dir.mkdir()
+    host_dir.mkdir()
+    _check_reduce_ranks(gpu, dev_dir, case, world, F, True, fused=fused, method="a2a")
+    _check_reduce_ranks(gpu, host_dir, case, world, F, False, fused=fused, method="a2a")
+    files = sorted(p.name for p in dev_dir.glob("*.npy"))
+    assert files and files == sorted(p.name for p in host_dir.glob("*.npy"))
+    for f in files:
+        assert np.array_equal(np.load(dev_dir / f), np.load(host_dir / f)), f
+
+
+def _check_reduce_ranks(gpu, tmp_path, case, world, F, dc, fused=False, method="ring"):
     import graphs
     from oracle import c_oracle
     from parity import assert_rows_close
@@ -264,7 +282,8 @@ def _check_reduce_ranks(gpu, tmp_path, case, world, F, dc, fused=False):
     uw, iw = graphs.embeddings(U, I, d, seed=K + d)
     ru, ri = c_oracle.lightgcn_forward(uw, iw, ei, K)
     torch.cuda.synchronize()
-    mp.spawn(_reduce_worker, args=(world, _free_port(), case, str(tmp_path), F, dc, fused), nprocs=world, join=True)
+    mp.spawn(_reduce_worker, args=(world, _free_port(), case, str(tmp_path), F, dc, fused, method), nprocs=world,
+             join=True)
     R = world // F
     shards = UserShards.build(np.bincount(ei[1], minlength=U + I), U, R)
     w = d // F

@@ -203,7 +203,8 @@ def test_grid_candidates():
     assert grid_candidates(2, 64) == [(1, 2, None)]
     # world >= 4: R - 1 >= 3 links; "reduce" (users sharded, items all-reduced) for every R > 1
     # peer sends (p2p) are timed after every other candidate (a hang there cannot stop the others)
-    red = lambda R, F: [(R, F, "reduce"), (R, F, "reduce-fused")]  # noqa: E731
+    red = lambda R, F: [(R, F, "reduce"), (R, F, "reduce-fused"), (R, F, "reduce-a2a"),  # noqa: E731
+                        (R, F, "reduce-a2a-fused")]
     rows_only = lambda w: [(w, 1, "allgather")] + red(w, 1)  # noqa: E731
     assert grid_candidates(4, 64) == [(1, 4, None), (2, 2, "allgather")] + red(2, 2) + rows_only(4) + \
         [(4, 1, "p2p")]
@@ -281,7 +282,7 @@ class CpuReducePlan:
         out_i[a:b] = (s / div) * mul
 
 
-def _reduce_worker(rank, world, port, kind, K, out_dir, F=1, fused=False):
+def _reduce_worker(rank, world, port, kind, K, out_dir, F=1, fused=False, method="ring"):
     import sys
 
     from conftest import PKG, ROOT
@@ -301,7 +302,7 @@ def _reduce_worker(rank, world, port, kind, K, out_dir, F=1, fused=False):
     plan = CpuReducePlan(ei, shards, g)
     uw, iw = graphs.embeddings(U, I, 16, seed=K)
     group = grid.exchange_group(dist)
-    red = ItemReducer(grid.R, group)
+    red = ItemReducer(grid.R, group, method=method)
     ou, oi = propagate_forward_reduced(torch.from_numpy(uw[:, c0:c1].copy()), torch.from_numpy(iw[:, c0:c1].copy()),
                                        plan, K, red, fused=fused)
     ua, ub = shards.users(g)
@@ -312,18 +313,20 @@ def _reduce_worker(rank, world, port, kind, K, out_dir, F=1, fused=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,world,K,F,fused", [("sym", 2, 3, 1, False), ("sub", 2, 3, 1, False),
-                                                  ("hub", 3, 4, 1, False), ("sym", 4, 2, 2, False),
-                                                  ("sub", 4, 1, 1, False), ("hub", 2, 3, 1, False),
-                                                  ("sub", 8, 3, 2, False), ("sym", 2, 0, 1, False),
-                                                  ("hub", 3, 4, 1, True), ("sub", 4, 1, 1, True),
-                                                  ("sub", 8, 3, 2, True)])
-def test_reduce_mode_matches_oracle(tmp_path, kind, world, K, F, fused):
+@pytest.mark.parametrize("kind,world,K,F,fused,method", [
+    ("sym", 2, 3, 1, False, "ring"), ("sub", 2, 3, 1, False, "ring"), ("hub", 3, 4, 1, False, "ring"),
+    ("sym", 4, 2, 2, False, "ring"), ("sub", 4, 1, 1, False, "ring"), ("hub", 2, 3, 1, False, "ring"),
+    ("sub", 8, 3, 2, False, "ring"), ("sym", 2, 0, 1, False, "ring"), ("hub", 3, 4, 1, True, "ring"),
+    ("sub", 4, 1, 1, True, "ring"), ("sub", 8, 3, 2, True, "ring"),
+    ("sub", 2, 3, 1, False, "a2a"), ("hub", 3, 4, 1, False, "a2a"), ("sub", 8, 3, 2, False, "a2a"),
+    ("sub", 4, 1, 1, True, "a2a"), ("sym", 4, 2, 2, True, "a2a")])
+def test_reduce_mode_matches_oracle(tmp_path, kind, world, K, F, fused, method):
     """The reduce mode (users sharded, item rows all-reduced per layer, the last layer
     reduce-scattered) over gloo: every row group's users and its share of the items within 1e-5
     per row of the one-rank oracle forward (an item row is the sum of R partial chains), the
     shares covering every item, and the pass order (the item rows' stack mean once, at the end);
-    fused: the layer's two passes issued as one pair."""
+    fused: the layer's two passes issued as one pair; a2a: the all_reduce as all_to_all + slice
+    sums in rank order + all_gather (ItemReducer method "a2a")."""
     import graphs
     from oracle import lgconv_ref as R
     from parity import assert_rows_close
@@ -332,7 +335,7 @@ def test_reduce_mode_matches_oracle(tmp_path, kind, world, K, F, fused):
 
     U, I, ei = _graph(kind)
     port = _free_port()
-    mp.spawn(_reduce_worker, args=(world, port, kind, K, str(tmp_path), F, fused), nprocs=world, join=True)
+    mp.spawn(_reduce_worker, args=(world, port, kind, K, str(tmp_path), F, fused, method), nprocs=world, join=True)
     uw, iw = graphs.embeddings(U, I, 16, seed=K)
     ref = R.lightgcn_forward(uw, iw, ei, K)
     ref = np.concatenate(ref) if isinstance(ref, tuple) else ref
