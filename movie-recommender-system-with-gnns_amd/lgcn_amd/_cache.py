@@ -47,15 +47,25 @@ def content_key(t: torch.Tensor, extra: tuple = ()) -> tuple:
 _KEYS: dict[int, tuple[weakref.ref, int, tuple]] = {}
 
 
+def _version(t: torch.Tensor):
+    """The in-place version counter, or None for an inference tensor (no counter: never memoised)."""
+    try:
+        return t._version
+    except RuntimeError:
+        return None
+
+
 def tensor_key(t: torch.Tensor) -> tuple:
     """content_key(t), memoised on the tensor object while it lives and is not modified in place."""
+    ver = _version(t)
     hit = _KEYS.get(id(t))
-    if hit is not None:
-        ref, ver, key = hit
-        if ref() is t and ver == t._version:
+    if hit is not None and ver is not None:
+        ref, v, key = hit
+        if ref() is t and v == ver:
             return key
     key = content_key(t)
-    _KEYS[id(t)] = (weakref.ref(t), t._version, key)
+    if ver is not None:
+        _KEYS[id(t)] = (weakref.ref(t), ver, key)
     if len(_KEYS) > 64 and len(_KEYS) % 64 == 0:  # amortised: drop the entries of freed tensors
         for k in [k for k, (r, _, _) in _KEYS.items() if r() is None]:
             del _KEYS[k]
@@ -64,7 +74,7 @@ def tensor_key(t: torch.Tensor) -> tuple:
 
 def _memo_hit(t: torch.Tensor) -> bool:
     hit = _KEYS.get(id(t))
-    return hit is not None and hit[0]() is t and hit[1] == t._version
+    return hit is not None and hit[0]() is t and hit[1] == _version(t)
 
 
 class ContentLRU:

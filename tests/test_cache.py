@@ -54,3 +54,11 @@ def test_extra_key_parts_separate_entries():
     assert c.get(a, lambda: "n5", extra=(5, 0)) == "n5"
     assert c.get(a, lambda: "n7", extra=(7, 0)) == "n7"
     assert c.get(a.clone(), lambda: "x", extra=(5, 0)) == "n5"
+
+
+def test_inference_tensors_are_keyed_by_content():
+    c = ContentLRU(4)
+    with torch.inference_mode():
+        a = torch.arange(6).view(2, 3)
+    assert c.get(a, lambda: 1) == 1
+    assert c.get(a.clone(), lambda: 2) == 1
