@@ -18,8 +18,10 @@
 // Rows live in two tables (r < split: lo[r], else hi[r - split]) like everywhere else.
 
 #include <climits>
+#include <cmath>
 
 #include "lgcn_common.h"
+#include "lgcn_exact.h"
 
 using namespace lgcn;
 
@@ -51,6 +53,10 @@ struct RowList {
 struct AdamK {
     float omb1, beta2, omb2, eps;
     int markstein;  // the step-constant division by Markstein's correction (div_step)
+    // zero-gradient replays in the exact shortened sqrt / division (fast_horizon) when set:
+    // 1 / -log2 of the per-step decay bounds of |m| and v (rounding included), host-computed
+    int fast;
+    float inv_lm, inv_lv;
 };
 
 template <class T>
@@ -97,6 +103,53 @@ __device__ __forceinline__ void adam_elem_zero(float& p, float& m, float& v, flo
     v = v * k.beta2;
     const float denom = div_step(sqrtf(v), bc2_sqrt, rc, k.markstein) + k.eps;
     p = p + step_size * (m / denom);
+}
+
+// adam_elem_zero with lgcn_exact.h's shortened sqrt and division: bitwise the same while every
+// operand stays in their ranges — v == +0 or v >= 2^-96, m == +0 or 2^-40 <= |m| <= 2^40, and the
+// denominator in [2^-40, 2^40] (eps >= 2^-40 and v <= 2^60 with c >= 2^-9, checked by the host and
+// by fast_horizon).
+__device__ __forceinline__ void adam_elem_zero_fast(float& p, float& m, float& v, float step_size, float bc2_sqrt,
+                                                    float rc, const AdamK& k) {
+    m = m - k.omb1 * m;
+    v = v * k.beta2;
+    const float denom = div_step(sqrt_normal(v), bc2_sqrt, rc, 1) + k.eps;
+    p = p + step_size * div_window(m, denom);
+}
+
+// How many zero-gradient replays from (m, v) stay inside adam_elem_zero_fast's ranges. A replay
+// multiplies |m| by at least f_m = (1 - omb1)(1 - 2^-22) and v by at least f_v = beta2 (1 - 2^-23)
+// (the two roundings of m - omb1 * m, the one of v * beta2), and makes neither larger, so from
+// |m| >= 2^e the first floor((e + 40) / -log2 f_m) replays keep |m| >= 2^-40 (inv_lm = 1 /
+// -log2 f_m, rounded down), likewise v >= 2^-96; +0 stays +0. 0 (never fast) for anything else:
+// |m| > 2^40, v > 2^60, a negative zero, NaN or inf.
+__device__ __forceinline__ int64_t horizon_m(float m, float inv) {
+    const uint32_t b = __float_as_uint(m);
+    if (b == 0u) return INT64_MAX;
+    const int e = static_cast<int>((b >> 23) & 0xffu) - 127;
+    if (e > 39 || e < -40) return 0;
+    return static_cast<int64_t>(static_cast<float>(e + 40) * inv);
+}
+
+__device__ __forceinline__ int64_t horizon_v(float v, float inv) {
+    const uint32_t b = __float_as_uint(v);
+    if (b == 0u) return INT64_MAX;
+    const int e = static_cast<int>((b >> 23) & 0xffu) - 127;
+    if ((b >> 31) || e > 59 || e < -96) return 0;
+    return static_cast<int64_t>(static_cast<float>(e + 96) * inv);
+}
+
+template <int NV>
+__device__ __forceinline__ int64_t fast_horizon(const float4 (&m)[NV], const float4 (&v)[NV], const AdamK& k) {
+    int64_t h = INT64_MAX;
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+        h = min(h, min(min(horizon_m(m[q].x, k.inv_lm), horizon_m(m[q].y, k.inv_lm)),
+                       min(horizon_m(m[q].z, k.inv_lm), horizon_m(m[q].w, k.inv_lm))));
+        h = min(h, min(min(horizon_v(v[q].x, k.inv_lv), horizon_v(v[q].y, k.inv_lv)),
+                       min(horizon_v(v[q].z, k.inv_lv), horizon_v(v[q].w, k.inv_lv))));
+    }
+    return h;
 }
 
 // Entry i of the list: its row, and whether it passes the first_b filter. An entry that fails it
@@ -194,9 +247,22 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
         m[q] = M[q * LPR];
         v[q] = V[q * LPR];
     }
+    // replays [from, fast_end) in the shortened arithmetic (bitwise the same), the rest in full
+    const int64_t fast_end = (k.fast && k.markstein && from <= upto) ? from + min(fast_horizon<NV>(m, v, k), upto - from + 1)
+                                                                     : from;
     for (int64_t s = from; s <= upto; ++s) {
         const float4 c = consts[s];
         const float rc = c.z;  // 1 / c.y, from lgcn_adam_consts
+        if (s < fast_end) {
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                adam_elem_zero_fast(p[q].x, m[q].x, v[q].x, c.x, c.y, rc, k);
+                adam_elem_zero_fast(p[q].y, m[q].y, v[q].y, c.x, c.y, rc, k);
+                adam_elem_zero_fast(p[q].z, m[q].z, v[q].z, c.x, c.y, rc, k);
+                adam_elem_zero_fast(p[q].w, m[q].w, v[q].w, c.x, c.y, rc, k);
+            }
+            continue;
+        }
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             adam_elem_zero(p[q].x, m[q].x, v[q].x, c.x, c.y, rc, k);
@@ -358,7 +424,16 @@ int lgcn_row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_l
         (n_a > 0 && !rows_a) || (n_b > 0 && !keys_b))
         return fail(LGCN_E_ARG, "lgcn_row_adam: bad args");
     RowList L{rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b};
-    const AdamK k{one_minus_beta1, beta2, one_minus_beta2, eps, beta2 == 0.999f};
+    AdamK k{one_minus_beta1, beta2, one_minus_beta2, eps, beta2 == 0.999f, 0, 0.0f, 0.0f};
+    // the shortened replay (adam_elem_zero_fast) needs the Markstein schedule (c >= sqrt(0.001)),
+    // a denominator floor eps in [2^-40, 2^30] and decays that shrink |m| and v
+    if (k.markstein && eps >= 0x1p-40f && eps <= 0x1p30f && one_minus_beta1 > 0.0f && one_minus_beta1 <= 0.5f) {
+        const double fm = (1.0 - static_cast<double>(one_minus_beta1)) * (1.0 - std::ldexp(1.0, -22));
+        const double fv = static_cast<double>(beta2) * (1.0 - std::ldexp(1.0, -23));
+        k.fast = 1;
+        k.inv_lm = static_cast<float>(1.0 / -std::log2(fm) * (1.0 - 1e-6));
+        k.inv_lv = static_cast<float>(1.0 / -std::log2(fv) * (1.0 - 1e-6));
+    }
     hipStream_t s = as_stream(stream);
     if (!al16(consts)) return fail(LGCN_E_ARG, "lgcn_row_adam: consts must be 16-byte aligned");
     const auto* c2 = reinterpret_cast<const float4*>(consts);

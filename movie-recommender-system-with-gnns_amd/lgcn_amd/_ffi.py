@@ -198,15 +198,17 @@ INCLUDE = _HERE.parent.parent / "include"
 # the translation units of liblgcn.so (lgcn_build.cpp carries the hash and is not hashed)
 SOURCES = ("lgcn_plan.hip", "lgcn_spmm.hip", "lgcn_optim.hip", "lgcn_bpr.hip", "lgcn_recall.hip", "lgcn_rowadam.hip",
            "lgcn_exchange.hip", "lgcn_partition.cpp", "lgcn_sample.cpp", "lgcn_tuning.cpp")
+# the headers they include (csrc/), hashed and tracked as build dependencies with include/lgcn.h
+HEADERS = ("lgcn_common.h", "lgcn_exact.h")
 
 
 def source_sha256() -> str:
-    """sha256 of the library's sources: each csrc translation unit, lgcn_common.h, include/lgcn.h
+    """sha256 of the library's sources: each csrc translation unit, the csrc headers, include/lgcn.h
     (name and bytes of each, in that order)."""
     import hashlib
 
     h = hashlib.sha256()
-    for f in [CSRC / s for s in SOURCES] + [CSRC / "lgcn_common.h", INCLUDE / "lgcn.h"]:
+    for f in [CSRC / s for s in SOURCES + HEADERS] + [INCLUDE / "lgcn.h"]:
         h.update(f.name.encode() + b"\0")
         h.update(f.read_bytes())
     return h.hexdigest()

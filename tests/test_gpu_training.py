@@ -227,22 +227,25 @@ def test_graph_replay_equals_eager(gpu):
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
 
 
-@pytest.mark.parametrize("clip", [None, 1.0])
-def test_row_lazy_adam_matches_dense_fused_adam(gpu, clip):
+@pytest.mark.parametrize("clip,d,betas", [(None, 64, (0.9, 0.999)), (1.0, 64, (0.9, 0.999)),
+                                           (None, 128, (0.8, 0.99)), (None, 512, (0.9, 0.999))])
+def test_row_lazy_adam_matches_dense_fused_adam(gpu, clip, d, betas):
     """RowLazyAdam (deferred rows replayed when touched, flush at the end) == dense
     FusedAdam(capturable=True) on the same sparse gradients: bitwise without clipping (the
     replays are the dense kernel's arithmetic with its per-step constants); with clipping the
-    norm is summed over other rows in another order, so to fp32 rounding of the clip coef."""
+    norm is summed over other rows in another order, so to fp32 rounding of the clip coef. betas
+    (0.8, 0.99): the step-constant division takes the IEEE division instead of the Markstein
+    shortcut (proven for beta2 = 0.999 only); d = 512: two float4 per lane."""
     from lgcn_amd.optim import FusedAdam, RowLazyAdam
 
-    U, I, d = 300, 200, 64
+    U, I = 300, 200
     N = U + I
     torch.manual_seed(0)
     w0 = [torch.randn(U, d, device=gpu) * 0.1, torch.randn(I, d, device=gpu) * 0.1]
     dense = [torch.nn.Parameter(t.clone()) for t in w0]
     lazy = [t.clone() for t in w0]
-    od = FusedAdam(dense, lr=1e-2, max_grad_norm=clip, capturable=True)
-    ol = RowLazyAdam(lazy[0], lazy[1], lr=1e-2, max_grad_norm=clip)
+    od = FusedAdam(dense, lr=1e-2, betas=betas, max_grad_norm=clip, capturable=True)
+    ol = RowLazyAdam(lazy[0], lazy[1], lr=1e-2, betas=betas, max_grad_norm=clip)
     rng = np.random.default_rng(1)
     for step in range(15):
         rows = np.unique(rng.integers(0, N, rng.integers(1, 120)))
