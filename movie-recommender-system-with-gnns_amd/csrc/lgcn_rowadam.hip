@@ -139,6 +139,8 @@ __device__ __forceinline__ int64_t horizon_v(float v, float inv) {
     return static_cast<int64_t>(static_cast<float>(e + 96) * inv);
 }
 
+constexpr int64_t kFastMinReplays = 3;
+
 template <int NV>
 __device__ __forceinline__ int64_t fast_horizon(const float4 (&m)[NV], const float4 (&v)[NV], const AdamK& k) {
     int64_t h = INT64_MAX;
@@ -247,9 +249,12 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
         m[q] = M[q * LPR];
         v[q] = V[q * LPR];
     }
-    // replays [from, fast_end) in the shortened arithmetic (bitwise the same), the rest in full
-    const int64_t fast_end = (k.fast && k.markstein && from <= upto) ? from + min(fast_horizon<NV>(m, v, k), upto - from + 1)
-                                                                     : from;
+    // replays [from, fast_end) in the shortened arithmetic (bitwise the same), the rest in full; a
+    // row with fewer than kFastMinReplays to replay skips it (the range checks cost about what two
+    // shortened replays save: the planted graph's rows are mostly one step behind)
+    const int64_t fast_end = (k.fast && k.markstein && upto - from + 1 >= kFastMinReplays)
+                                 ? from + min(fast_horizon<NV>(m, v, k), upto - from + 1)
+                                 : from;
     for (int64_t s = from; s <= upto; ++s) {
         const float4 c = consts[s];
         const float rc = c.z;  // 1 / c.y, from lgcn_adam_consts
