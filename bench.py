@@ -296,9 +296,18 @@ def parse_tune(items) -> dict:
         if k not in types:
             raise SystemExit(f"--tune: unknown field {k!r} (fields: {', '.join(types)})")
         t = types[k]
+        if v == "None" and "None" in t:
+            out[k] = None
+            continue
         out[k] = (v not in ("0", "false", "False") if "bool" in t else
-                  (None if v == "None" else float(v)) if "float" in t else int(v) if "int" in t else v)
+                  float(v) if "float" in t else int(v) if "int" in t else v)
     return out
+
+
+def _batch_chunk_for(edges: int) -> int:
+    from lgcn_amd.train_step import batch_chunk_for
+
+    return batch_chunk_for(edges)
 
 
 def apply_tune(tuned: dict) -> None:
@@ -1109,6 +1118,7 @@ def run_train(args):
                            ("fused sparse step" + ("" if (args.no_graphs or args.torch_adam) else ", hipGraph per batch")),
                    "parts_per_batch": q, "f_intra": f_intra, "layers": K, "dim": d, "num_users": U,
                    "num_items": I, "train_edges": n_tr,
+                   "batch_plan_chunks": sorted({_batch_chunk_for(int(b.edge_index.shape[1])) for b in batches}),
                    "parallelism": (f"columns{world}: every rank the same batches and negatives on {d // world} of "
                                    f"{d} columns; one all_reduce of the triplets' [B, 6] dots/norms and one "
                                    f"all_gather of the clip norm's partials per step (the one-GPU step's semantics)"

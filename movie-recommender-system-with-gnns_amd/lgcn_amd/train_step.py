@@ -141,6 +141,25 @@ class _SegmentedGraph:
                 self.colls[i]()
 
 
+def batch_chunk_for(edges: int) -> int:
+    """Hub chunk of a batch's propagation plan. Short chunks while the batch is small (its item
+    passes are latency chains: more, shorter chains), longer ones for the big intra-part batches of
+    a structured graph (fewer partials and block-split chains). Measured, K=3, d=128 (ms per step,
+    profiles/r05y_batch_chunk/): 20k edges 0.162 / 0.163 / 0.177 at 16 / 32 / 64; 80-90k edges
+    0.385 / 0.395 / 0.418 and 0.340 / 0.347 / 0.381 at 32 / 64 / 128; 360k edges 0.489 / 0.464 /
+    0.456 / 0.456 / 0.459 at 32 / 64 / 128 / 256 / 512. lgcn_amd.tuning's batch_chunk forces one."""
+    from . import tuning
+
+    forced = tuning.get().batch_chunk
+    if forced is not None:
+        return int(forced)
+    if edges >= 240_000:
+        return 128
+    if edges >= 160_000:
+        return 64
+    return 32
+
+
 class _BatchState:
     def __init__(self, model, edge_index: torch.Tensor, d: int, lazy: bool = False):
         dev = edge_index.device
@@ -148,8 +167,8 @@ class _BatchState:
         N = U + I
         from .plan import PropagationPlan
 
-        # short chunks: a batch has few edges, so latency (not bandwidth) bounds its item passes
-        self.plan = PropagationPlan(edge_index, N, 32, side_split=U, touched_only=True)
+        self.plan = PropagationPlan(edge_index, N, batch_chunk_for(int(edge_index.shape[1])), side_split=U,
+                                    touched_only=True)
         src, dst = edge_index[0], edge_index[1]
         self.users = src[src < U].contiguous()
         self.pos = (dst[dst >= U] - U).contiguous()

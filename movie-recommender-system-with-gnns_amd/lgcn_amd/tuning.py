@@ -39,6 +39,9 @@ class Tuning:
     neg_grouping: str = "count"
     # batch size from which the negatives take the sorted scatter instead of the range scatter
     sorted_scatter_min_b: int = 49152
+    # hub chunk (edges per lane-group chain) of a Cluster-GCN batch's propagation plan: None =
+    # lgcn_amd.train_step.batch_chunk_for's measured rule (by the batch's edge count); > 0 = forced
+    batch_chunk: int | None = None
     # Recall@k: candidates in the strided subset that sets the first thresholds
     recall_subset: int = 16384
     # utils.train_test.train routes eligible calls to the fused batch step (False: reference loop)
@@ -60,6 +63,8 @@ class Tuning:
             raise ValueError(f"neg_grouping must be 'count' or 'radix', got {self.neg_grouping!r}")
         if self.sorted_scatter_min_b < 1 or self.recall_subset < 1:
             raise ValueError("sorted_scatter_min_b and recall_subset must be >= 1")
+        if self.batch_chunk is not None and self.batch_chunk < 1:
+            raise ValueError(f"batch_chunk must be None or >= 1, got {self.batch_chunk}")
 
 
 _current = Tuning()
