@@ -142,7 +142,8 @@ class _SegmentedGraph:
 
 
 def batch_chunk_for(edges: int) -> int:
-    """Hub chunk of a batch's propagation plan. Short chunks while the batch is small (its item
+    """Hub chunk of a batch's propagation plan (edges: the batch's directed edges) and of its fixed
+    gradient rows' segment plans (edges: their 2B contributions). Short chunks while the batch is small (its item
     passes are latency chains: more, shorter chains), longer ones for the big intra-part batches of
     a structured graph (fewer partials and block-split chains). Measured, K=3, d=128 (ms per step,
     profiles/r05y_batch_chunk/): 20k edges 0.162 / 0.163 / 0.177 at 16 / 32 / 64; 80-90k edges
@@ -190,10 +191,10 @@ class _BatchState:
         if self.lazy:
             # row-lazy optimizer: only the batch's touched rows (and the negatives) are written
             self.fixed_dense, self.fixed_sparse, self.fixed_touched = segment_directions(
-                self.keys[:2 * B], N, chunk=32, row_mask=self.plan.touched)
+                self.keys[:2 * B], N, chunk=batch_chunk_for(2 * B), row_mask=self.plan.touched)
             self.touched_rows = torch.nonzero(self.plan.touched).squeeze(1).to(torch.int32).contiguous()
         elif self.small:
-            self.fixed_dense, self.fixed_sparse = segment_directions(self.keys[:2 * B], N, chunk=32)
+            self.fixed_dense, self.fixed_sparse = segment_directions(self.keys[:2 * B], N, chunk=batch_chunk_for(2 * B))
         if self.small and B >= sorted_scatter_min_b():
             # large B: the negatives are grouped by row once per step and scattered row by row
             # (lgcn_sorted_scatter_add); the grouping is a counting sort (lgcn_group_keys) or,
