@@ -52,8 +52,9 @@ def slice_bytes_for(num_nodes: int, d: int) -> int:
     """Source-slice size for a full-graph propagation of width d (0 = no slicing). Measured on
     the C2 graph (tools/sliced_probe.py, profiles/r01g_sliced): slicing pays while the gathered
     table is small enough that re-reading the running row sums once per slice costs less than the
-    cache misses it saves — about 8 slices of 8–24 MB for tables of 16–512 MB; beyond that (C5:
-    11 GB) the plain schedule is faster. PropagationPlan.schedule also requires >= 8 edges per
+    cache misses it saves — about 8 slices of 8–24 MB for tables of 16–512 MB, 2-3 slices of 4-12
+    MB for the 4-32 MB tables of the narrow column shares (d = 8-32); beyond 512 MB (C5: 11 GB)
+    the plain schedule is faster. PropagationPlan.schedule also requires >= 8 edges per
     row per slice. lgcn_amd.tuning's slice_mb overrides the size and that density test (0
     disables)."""
     from . import tuning
@@ -62,12 +63,22 @@ def slice_bytes_for(num_nodes: int, d: int) -> int:
     if v is not None:
         return int(v * 2**20) if v > 0 else 0
     x = int(num_nodes) * int(d) * 4
-    if x < 16 * 2**20 or x > 512 * 2**20:
+    if x < 4 * 2**20 or x > 512 * 2**20:
         return 0
+    if x < 8 * 2**20:
+        # 4-8 MB tables (C2 at d = 8, the 1 x 8 grid's column share): 4 MB slices (bench.py --dim 8:
+        # 0.775 plain -> 0.721 ms; 3 MB 0.727, 6 MB 0.731, profiles/r05zd_narrow/)
+        return 4 * 2**20
+    if x < 16 * 2**20:
+        # 8-16 MB tables (C2 at d = 16, the 1 x 4 grid's column share): 8 MB slices, 2 user + 1
+        # item (bench.py --dim 16: 0.6175 plain -> 0.6026 ms per K=3 step; 6 MB 0.6020, 12 MB
+        # 0.6122, profiles/r05zd_narrow/)
+        return 8 * 2**20
     if x < 32 * 2**20:
         # 16-32 MB tables (C2 at d = 32, the 1 x 2 grid's column share): 12 MB slices, i.e. 2 user +
         # 1 item slice, beat 8 MB's 3 + 1 (bench.py --dim 32: 0.710 -> 0.690 ms per K=3 step,
-        # profiles/r02zz_narrow/); below 16 MB (d = 16) the plain schedule stays ahead
+        # profiles/r02zz_narrow/; round 5: 0.667 at 12 MB vs 0.686 / 0.671 / 0.751 / 0.791 at 8 /
+        # 16 / 24 MB / plain, profiles/r05zd_narrow/)
         return 12 * 2**20
     return int(min(max(x // 8, 8 * 2**20), 24 * 2**20))
 
