@@ -499,6 +499,8 @@ def main():
     ap.add_argument("--no-graphs", action="store_true", help="train: run the fused step eagerly (no hipGraph replay)")
     ap.add_argument("--exchange", action="store_true",
                     help="train, N=1: run the row exchange anyway (measures its kernels; N>1 always uses it)")
+    ap.add_argument("--dp-lr", choices=["sqrt", "same"], default="sqrt",
+                    help="train, data parallel: Adam lr 1e-3 * sqrt(W) (default; lgcn_amd.distributed.dp_lr) or 1e-3")
     ap.add_argument("--dp-mode", choices=["auto", "replicated", "owner", "columns"], default="auto",
                     help="train, N > 1: column-sharded exact training (every rank the same batches on d/N "
                          "columns, one [B, 6] all_reduce per step — the one-GPU step's semantics, so Recall is "
@@ -1003,17 +1005,20 @@ def run_train(args):
             model.user_embedding.weight.copy_(full.user_embedding.weight[:, c0:c1])
             model.item_embedding.weight.copy_(full.item_embedding.weight[:, c0:c1])
         del full
+    # data parallel (W parts per Adam step): lr * sqrt(W), the rule that keeps Recall@20 and @100 on
+    # the reference's (lgcn_amd.distributed.dp_lr); columns and one GPU: the reference's 1e-3
+    lr = D.dp_lr(1e-3, world) if (world > 1 and cols is None and args.dp_lr == "sqrt") else 1e-3
     if args.torch_adam:
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+        opt = torch.optim.Adam(model.parameters(), lr=lr)
     elif lazy:
         from lgcn_amd.optim import RowLazyAdam
 
-        opt = RowLazyAdam(model.user_embedding.weight.data, model.item_embedding.weight.data, lr=1e-3,
+        opt = RowLazyAdam(model.user_embedding.weight.data, model.item_embedding.weight.data, lr=lr,
                           max_grad_norm=1)
     else:
         from lgcn_amd.optim import FusedAdam
 
-        opt = FusedAdam(model.parameters(), lr=1e-3, max_grad_norm=1, capturable=not args.autograd,
+        opt = FusedAdam(model.parameters(), lr=lr, max_grad_norm=1, capturable=not args.autograd,
                         keep_clipped_grad=False)
     params = list(model.parameters())
     torch.manual_seed(1000 + rank)
@@ -1146,8 +1151,10 @@ def run_train(args):
                                       "columns each; Recall@20/@100 equal the one-GPU run's (asserted within "
                                       "+-0.002 of the reference harness)"}
         if cols is not None else
-        {"mode": dp_mode, "status": f"data parallel: W = {world} parts per Adam step; Recall@20 asserted within "
-                                    "+-0.002 at W = 8 (round 3: 0.0015-0.0018), Recall@100 outside (0.0030-0.0032)"}
+        {"mode": dp_mode, "lr": lr,
+         "status": f"data parallel: W = {world} parts per Adam step at lr 1e-3 * sqrt(W) (--dp-lr sqrt); C1 size "
+                   "at W = 8: |dRecall@20| 0.00015, |dRecall@100| 0.00025 (both asserted within +-0.002); at "
+                   "lr 1e-3 (--dp-lr same) 0.0015 / 0.0030 (Recall@100 outside)"}
         if world > 1 else
         {"mode": "single GPU", "status": "the reference schedule; C1-size |dRecall@20| 0.00037 (asserted <= 0.002)"})
     if rank == 0:

@@ -35,6 +35,19 @@ def device_collectives(group=None) -> bool:
     return dist.get_backend(group) == "nccl"
 
 
+def dp_lr(lr: float, world: int) -> float:
+    """The Adam learning rate for data-parallel training over `world` ranks: lr * sqrt(world).
+
+    A data-parallel step averages `world` parts' gradients, so an epoch takes `world` times fewer
+    (and less noisy) Adam steps than the reference's one-part-per-step loop (reference
+    utils/train_test.py:86-101); at the reference's lr the model then trails it. Measured on the C1
+    graph against the reference harness (tools/dp_lr_probe.py, profiles/r05zg_dp_lr/: |dRecall@20|
+    / |dRecall@100| at W = 8, 5 epochs): lr x1 0.0015 / 0.0030 (Recall@100 outside the +-0.002
+    band), x sqrt(8) 0.00015 / 0.00025, x8 0.0008 / 0.0008; sqrt(W) is also the closest at W = 2
+    and 4 and at 10 epochs (all within 0.0005 on both metrics)."""
+    return float(lr) * float(world) ** 0.5
+
+
 def world_info():
     if dist.is_available() and dist.is_initialized():
         return dist.get_world_size(), dist.get_rank()

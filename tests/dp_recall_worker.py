@@ -13,7 +13,9 @@ reference's schedule — every part, one per step, the same negatives — on its
 tables are gathered to rank 0 for Recall. MODE "plain": the same schedule and negatives without
 the column split (W = 1).
 
-python tests/dp_recall_worker.py RANK WORLD PORT OUT EPOCHS PARTS [MODE: dp | cols | plain]"""
+LR_SCALE (dp only, default 1): the data-parallel Adam's lr is 1e-3 * LR_SCALE (tools/dp_lr_probe.py).
+
+python tests/dp_recall_worker.py RANK WORLD PORT OUT EPOCHS PARTS [MODE: dp | cols | plain] [LR_SCALE]"""
 import json
 import os
 import sys
@@ -78,6 +80,7 @@ def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
     epochs, parts = int(sys.argv[5]), int(sys.argv[6])
     mode = sys.argv[7] if len(sys.argv) > 7 else "dp"
+    lr_scale = float(sys.argv[8]) if len(sys.argv) > 8 and mode == "dp" else 1.0
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -107,7 +110,8 @@ def main():
     with torch.no_grad():
         m.user_embedding.weight.copy_(ref_init.user_embedding.weight[:, c0:c1])
         m.item_embedding.weight.copy_(ref_init.item_embedding.weight[:, c0:c1])
-    opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-3, max_grad_norm=1.0)
+    opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-3 * lr_scale,
+                      max_grad_norm=1.0)
     if mode == "dp":
         ex = D.RowExchange(D.exchange_capacity(batches, U), U + I, 64, gpu, world) if world > 1 else None
         step = FusedTrainStep(m, opt, world=world, lazy=True, exchange=ex, neg_seed=1000 + rank)
