@@ -274,6 +274,56 @@ def test_row_lazy_adam_matches_dense_fused_adam(gpu, clip, d, betas):
             assert (a.detach() - b).abs().max().item() <= 1e-6 * a.abs().max().item()
 
 
+@pytest.mark.parametrize("d", [64, 128])
+def test_row_lazy_adam_long_gaps_bitwise_dense(gpu, d):
+    """Rows left untouched for ~300 steps are bitwise the dense FusedAdam after their catch-up and
+    the flush: the zero-gradient replays take csrc/lgcn_exact.h's shortened sqrt / division only
+    while a per-row bound keeps |m| >= 2^-40 and v >= 2^-96, and the full sequences after. The
+    rows are chosen to cross that bound mid-replay (touched at the first and last step only: |m|
+    from ~1e-3 decays by 0.9 a step, past 2^-40 after ~200 steps; a flush at step 160 splits the
+    gap), to start below it (first gradient ~1e-14: |m| ~1e-15), to stay at exact zero (no
+    nonzero gradient ever), and to be touched every step or at random."""
+    from lgcn_amd.optim import FusedAdam, RowLazyAdam
+
+    U, I = 40, 24
+    N = U + I
+    torch.manual_seed(3)
+    w0 = [torch.randn(U, d, device=gpu) * 0.1, torch.randn(I, d, device=gpu) * 0.1]
+    dense = [torch.nn.Parameter(t.clone()) for t in w0]
+    lazy = [t.clone() for t in w0]
+    od = FusedAdam(dense, lr=1e-2, max_grad_norm=None, capturable=True)
+    ol = RowLazyAdam(lazy[0], lazy[1], lr=1e-2, max_grad_norm=None, max_steps=1024)
+    rng = np.random.default_rng(2)
+    steps = 320
+    scale = np.ones(N)
+    scale[0:10] = 1e-2      # ordinary rows
+    scale[10:20] = 1e-14    # |m| below the fast range from the start
+    scale[20:24] = 0.0      # never a nonzero gradient: m = v = 0 throughout
+    busy = np.array([30, 31, U + 3, U + 4])  # touched every step
+    for step in range(steps):
+        if step == 0 or step == steps - 1:
+            rows = np.arange(N)
+        else:
+            rows = np.unique(np.concatenate([busy, rng.integers(24, N, 3)]))  # rows 0..23 idle
+        gfull = torch.zeros(N, d, device=gpu)
+        gr = torch.randn(len(rows), d, device=gpu) * torch.from_numpy(scale[rows]).float().to(gpu)[:, None]
+        gfull[torch.from_numpy(rows).to(gpu)] = gr
+        dense[0].grad, dense[1].grad = gfull[:U].clone(), gfull[U:].clone()
+        ra = torch.from_numpy(rows.astype(np.int32)).to(gpu)
+        ol.catch_up(ra)
+        ol.gu.copy_(gfull[:U])
+        ol.gi.copy_(gfull[U:])
+        ol.step_rows(ra)
+        od.step()
+        if step == steps // 2:  # a mid-run flush: every row current, then the gaps resume
+            ol.flush()
+            for a, b in zip(dense, lazy):
+                assert torch.equal(a.detach(), b)
+    ol.flush()
+    for a, b in zip(dense, lazy):
+        assert torch.equal(a.detach(), b)
+
+
 @pytest.mark.parametrize("use_graphs,clip,whole", [(False, float("inf"), False), (True, float("inf"), False),
                                                    (False, 1e6, False), (True, 1e6, True), (False, 1.0, False)])
 def test_lazy_train_step_matches_dense_step(gpu, use_graphs, clip, whole):
