@@ -1029,7 +1029,7 @@ def run_train(args):
         from lgcn_amd import _ffi
         from lgcn_amd.owner import OwnerExchange, owner_capacity
 
-        exchange = OwnerExchange(owner_capacity(batches, U, world), N, d, dev, world, rank,
+        exchange = OwnerExchange(owner_capacity(batches, U, world, num_items=I), N, d, dev, world, rank,
                                  _ffi.load().lgcn_row_grad_norm_workspace_floats())
         log(f"[rank {rank}] owner exchange: {exchange.cap} slots per destination, blocks of "
             f"{exchange.blk * 4 / 1e6:.2f} MB, two all_to_alls per step")

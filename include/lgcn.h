@@ -38,7 +38,7 @@ extern "C" {
 
 typedef void* lgcn_stream_t; /* a hipStream_t; NULL = the null stream */
 
-#define LGCN_ABI_VERSION 7
+#define LGCN_ABI_VERSION 8
 
 #define LGCN_OK 0
 #define LGCN_E_ARG (-1)         /* bad size / null pointer / unsupported argument */
@@ -625,7 +625,10 @@ int lgcn_rows_accumulate(const int64_t* ids, const float* rows, int64_t world, i
  *     destination sets *overflow |= 1 (the row is dropped: the caller must check).
  *   lgcn_owner_pack_requests: each listed row id (rows_a, then keys_b + off_b; duplicates allowed)
  *     into destination row % world's request slots (counts[world + o]) and mine[o*rcap + slot];
- *     full: *overflow |= 2.
+ *     full: *overflow |= 2. claim (nullable, int32[N]; ABI 8): each distinct row requested once —
+ *     stamp (>= 0) must differ from every value claim held before the call (callers keep claim at
+ *     -1 initially and pass an increasing stamp), so a destination needs at most its share of
+ *     the distinct rows (a structured graph's large batches draw each item many times).
  *   lgcn_rows_gather: rows[i] = p[ids[i]] for ids[i] >= 0 (scatter != 0: p[ids[i]] = rows[i]).
  *   lgcn_rows_mark: mask[ids[i]] = value for ids[i] >= 0 (and first[i], if first is given).
  * Replaces the same reference step as lgcn_rows_pack (utils/train_test.py:92-96 under DP). */
@@ -637,7 +640,8 @@ int lgcn_owner_pack_rows(const float* g_lo, const float* g_hi, int64_t split, in
                          float* send, int32_t* overflow, lgcn_stream_t stream);
 int lgcn_owner_pack_requests(const int32_t* rows_a, int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b,
                              int64_t world, int64_t rcap, int64_t block_floats, int64_t req_off, int32_t* counts,
-                             float* send, int64_t* mine, int32_t* overflow, lgcn_stream_t stream);
+                             float* send, int64_t* mine, int32_t* overflow, int32_t* claim, int32_t stamp,
+                             lgcn_stream_t stream);
 int lgcn_rows_gather(const float* p_lo, const float* p_hi, int64_t split, int32_t d, const int64_t* ids, int64_t n,
                      float* rows, int32_t scatter, lgcn_stream_t stream);
 int lgcn_rows_mark(const int64_t* ids, const uint8_t* first, int64_t n, uint8_t* mask, int32_t value,

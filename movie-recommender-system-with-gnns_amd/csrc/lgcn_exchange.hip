@@ -183,14 +183,19 @@ __global__ __launch_bounds__(kBlock) void k_owner_pack_rows(
 }
 
 // Request ids (rows_a, then keys_b + off_b) to destination row % W; also mine[o*rcap + slot].
+// claim (nullable): each distinct row is requested once — the entry whose exchange of the call's
+// stamp into claim[row] finds another value packs it, the others skip (a row's copy is the same
+// whichever entry requested it).
 __global__ void k_owner_pack_requests(const int32_t* __restrict__ rows_a, int64_t n_a,
                                       const int64_t* __restrict__ keys_b, int64_t n_b, int64_t off_b, int64_t world,
                                       int64_t rcap, int64_t block_floats, int64_t req_off,
                                       int32_t* __restrict__ counts, float* __restrict__ send,
-                                      int64_t* __restrict__ mine, int32_t* __restrict__ overflow) {
+                                      int64_t* __restrict__ mine, int32_t* __restrict__ overflow,
+                                      int32_t* __restrict__ claim, int32_t stamp) {
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n_a + n_b; i += stride) {
         const int64_t row = i < n_a ? int64_t(rows_a[i]) : keys_b[i - n_a] + off_b;
+        if (claim && atomicExch(claim + row, stamp) == stamp) continue;  // already requested this call
         const int64_t o = row % world;
         const int slot = atomicAdd(counts + world + o, 1);
         if (slot >= rcap) {
@@ -303,13 +308,16 @@ int lgcn_owner_pack_rows(const float* g_lo, const float* g_hi, int64_t split, in
 
 int lgcn_owner_pack_requests(const int32_t* rows_a, int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b,
                              int64_t world, int64_t rcap, int64_t block_floats, int64_t req_off, int32_t* counts,
-                             float* send, int64_t* mine, int32_t* overflow, lgcn_stream_t stream) {
+                             float* send, int64_t* mine, int32_t* overflow, int32_t* claim, int32_t stamp,
+                             lgcn_stream_t stream) {
     if (!send || !counts || !mine || !overflow || world < 1 || rcap < 0 || n_a < 0 || n_b < 0 ||
-        (n_a > 0 && !rows_a) || (n_b > 0 && !keys_b) || block_floats < req_off + 2 * rcap || (req_off & 1))
+        (n_a > 0 && !rows_a) || (n_b > 0 && !keys_b) || block_floats < req_off + 2 * rcap || (req_off & 1) ||
+        (claim && stamp < 0))
         return fail(LGCN_E_ARG, "lgcn_owner_pack_requests: bad args");
     if (n_a + n_b == 0) return LGCN_OK;
     k_owner_pack_requests<<<grid_for(n_a + n_b, kBlock, 4096), kBlock, 0, as_stream(stream)>>>(
-        rows_a, n_a, keys_b, n_b, off_b, world, rcap, block_floats, req_off, counts, send, mine, overflow);
+        rows_a, n_a, keys_b, n_b, off_b, world, rcap, block_floats, req_off, counts, send, mine, overflow, claim,
+        stamp);
     return check_launch("k_owner_pack_requests");
 }
 

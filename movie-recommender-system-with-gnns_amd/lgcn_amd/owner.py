@@ -40,18 +40,26 @@ from . import _ffi
 from .distributed import device_collectives
 
 
-def owner_capacity(batches, num_users: int, world: int, slack: float = 1.25, floor: int = 64) -> int:
+def owner_capacity(batches, num_users: int, world: int, slack: float = 1.25, floor: int = 64,
+                   num_items: int | None = None) -> int:
     """Slots per destination block (gradient rows, and request ids): the most touched rows any
-    batch has on one owner plus its negatives' expected share with slack (uniform negatives over
-    the items: Binomial(B, 1/W) never comes near 1.25x its mean + 64 at these sizes), even, agreed
-    across ranks. A full destination is flagged (check_overflow), never silently wrapped."""
+    batch has on one owner plus its negatives' share — in expectation B / W with slack (uniform
+    negatives over the items: Binomial(B, 1/W) never comes near 1.25x its mean + 64 at these
+    sizes), and at most the owner's items (row r is owned by rank r % W: ceil(I / W) of them),
+    since both lists carry each distinct row once (gradient rows: first occurrences; requests:
+    lgcn_owner_pack_requests' claim) — pass num_items for that bound (a structured graph's large
+    batches: planted C3 at W = 8, 29k -> 8.3k slots). Even, agreed across ranks. A full
+    destination is flagged (check_overflow), never silently wrapped."""
     cap = 0
     for b in batches:
         ei = b.edge_index
         touched = torch.unique(ei)
         per_owner = torch.bincount(touched % world, minlength=world).max().item() if touched.numel() else 0
         B = int((ei[0] < num_users).sum())
-        cap = max(cap, int(per_owner) + int(np.ceil(B / world * slack)) + floor)
+        neg = int(np.ceil(B / world * slack)) + floor
+        if num_items is not None:
+            neg = min(neg, -(-int(num_items) // world))
+        cap = max(cap, int(per_owner) + neg)
     if dist.is_available() and dist.is_initialized() and world > 1:
         t = torch.tensor([cap], dtype=torch.int64)
         if device_collectives():
@@ -99,6 +107,9 @@ class OwnerExchange:
                 raise ValueError(f"OwnerExchange: norm_parts={self.norm_parts} != the kernel's {need} partials")
         self.partials = torch.zeros(self.norm_parts, dtype=torch.float32, device=device)
         self.partials_all = torch.zeros(W * self.norm_parts, dtype=torch.float32, device=device)
+        # request dedupe (lgcn_owner_pack_requests' claim): -1, then one increasing stamp per call
+        self.req_claim = torch.full((self.N,), -1, dtype=torch.int32, device=device)
+        self.req_stamp = 0
         self.nccl = W > 1 and device_collectives()
         self.bytes = 0  # received from peers over the run (self blocks excluded)
         self.pending = None  # the batch state whose rows the last step requested

@@ -661,10 +661,15 @@ class FusedTrainStep:
         ex.mine.fill_(-1)
         if nxt is not None:
             self._draw(nxt, self._k + 1)
+            ex.req_stamp = (ex.req_stamp + 1) % (2**31 - 1)
+            if ex.req_stamp == 0:  # wrapped: no stale stamp may equal a new one
+                ex.req_claim.fill_(-1)
+                ex.req_stamp = 1
             _ffi.check(lib.lgcn_owner_pack_requests(nxt.touched_rows.data_ptr(), nxt.touched_rows.numel(),
                                                     nxt.neg.data_ptr(), nxt.B, U, ex.world, ex.rcap, ex.blk,
                                                     ex.req_off, ex.counts.data_ptr(), ex.send.data_ptr(),
-                                                    ex.mine.data_ptr(), ex.overflow.data_ptr(), stream),
+                                                    ex.mine.data_ptr(), ex.overflow.data_ptr(),
+                                                    ex.req_claim.data_ptr(), ex.req_stamp, stream),
                        "lgcn_owner_pack_requests")
         ex.exchange_blocks()
         graphs_ok = use_graphs and self._owner_graphs is not None
@@ -700,9 +705,9 @@ class FusedTrainStep:
         self._synced = False
         self._k += 1
         if not getattr(st, "owner_checked", False):
-            # the blocks are sized so that neither list can overflow (cap >= touched + B of every
-            # batch); the first step of each batch state checks that with one host read, so a
-            # dropped row is an error at once rather than at the next check_overflow()
+            # the blocks are sized so that neither list overflows (owner_capacity); the first step
+            # of each batch state checks that with one host read, so a dropped row is an error at
+            # once rather than at the next check_overflow()
             ex.check_overflow()
             st.owner_checked = True
         return loss

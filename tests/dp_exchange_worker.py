@@ -60,7 +60,7 @@ def main():
     cap = D.exchange_capacity(batches, U)
     from lgcn_amd.owner import OwnerExchange, owner_capacity
 
-    ocap = owner_capacity(batches, U, world)
+    ocap = owner_capacity(batches, U, world, num_items=I)
     variants = os.environ.get("DP_VARIANTS", "dense,lazy,lazy_graphs,owner,owner_graphs").split(",")
     res = {}
     clip_ = None if clip == 0 else clip

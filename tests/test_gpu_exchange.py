@@ -249,6 +249,38 @@ def test_dp8_owner_exchange_matches_replicated(gpu, tmp_path, clip):
           f"owner {res[0]['owner']['bytes_per_step'] / 1e6:.3f} MB (cap {res[0]['cap']}, owner cap {res[0]['ocap']})")
 
 
+def test_dp8_owner_exchange_dense_batches_matches_replicated(gpu, tmp_path):
+    """Batches with many more triplets than items (each part's users draw every item several
+    times as negatives — the planted graph's case): the owner-sharded exchange requests each
+    distinct row once (lgcn_owner_pack_requests' claim, ABI 8), so its blocks are sized by the
+    owner's items (owner_capacity(num_items=I)) rather than by its share of the triplets — and it
+    stays bitwise the replicated exchange without clipping, with identical tables on every rank."""
+    from lgcn_amd import cluster as C
+    from lgcn_amd import synth
+    from lgcn_amd.owner import owner_capacity
+
+    g = synth.bipartite(640, 48, 9000, seed=5)
+    U, I = g.num_users, g.num_items
+    part = C.partition_nodes(g.edge_index, g.num_nodes, 8)
+    lists = [x for x in C.intra_part_edges(g.edge_index, part, 8) if x.shape[1]]
+    B = [int((x[0] < U).sum()) for x in lists]
+    assert min(B) > I  # every batch draws more negatives than there are items
+    batches = [_Batch(torch.from_numpy(x)) for x in lists]
+    assert owner_capacity(batches, U, 8, num_items=I) < owner_capacity(batches, U, 8)
+    npz = tmp_path / "dense_batches.npz"
+    np.savez(npz, U=U, I=I, **{f"b{i}": x for i, x in enumerate(lists)})
+    res = _spawn(8, tmp_path, float("inf"), "lazy,owner,owner_graphs", steps=16, npz=str(npz))
+    for name in ("lazy", "owner", "owner_graphs"):
+        for r in range(1, 8):
+            assert torch.equal(res[0][name]["user"], res[r][name]["user"]), (name, r)
+            assert torch.equal(res[0][name]["item"], res[r][name]["item"]), (name, r)
+    for r in range(8):
+        _check_owner_vs_replicated(res[r], float("inf"))
+    print(f"dense batches (B {min(B)}-{max(B)} > I {I}), W=8: owner cap {res[0]['ocap']} "
+          f"(without the item bound {owner_capacity(batches, U, 8)}), bytes received per rank per step: "
+          f"replicated {res[0]['lazy']['bytes_per_step'] / 1e6:.3f} MB, owner {res[0]['owner']['bytes_per_step'] / 1e6:.3f} MB")
+
+
 @pytest.mark.parametrize("world,clip", [(2, float("inf")), (2, 1.0), (4, 1.0)])
 def test_column_sharded_graph_replay_matches_eager(gpu, tmp_path, world, clip):
     """Column-sharded training captured per batch as graphs cut at its two collectives

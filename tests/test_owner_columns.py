@@ -24,6 +24,29 @@ def _free_port():
     return p
 
 
+def test_owner_capacity_bounded_by_the_owners_items():
+    """A batch with more triplets than items (the planted graph's 180k triplets over 59k items):
+    each destination carries each distinct row once (first-occurrence gradient rows, claimed
+    requests), so given num_items its block needs its touched rows plus at most its ceil(I / W)
+    items, not its share of B."""
+    from lgcn_amd.owner import owner_capacity
+
+    rng = np.random.default_rng(1)
+    U, I = 400, 30
+    u = rng.integers(0, U, 2000)
+    i = rng.integers(0, I, 2000) + U
+    ei = np.unique(np.stack([np.concatenate([u, i]), np.concatenate([i, u])]), axis=1)
+    b = _Batch(torch.from_numpy(ei))
+    assert int((ei[0] < U).sum()) > I
+    t = np.unique(ei)
+    for W in (2, 4, 8):
+        per_owner = int(np.bincount(t % W, minlength=W).max())
+        cap = owner_capacity([b], U, W, num_items=I)
+        want = per_owner + -(-I // W)
+        assert cap == want + want % 2
+        assert cap < owner_capacity([b], U, W)
+
+
 def test_owner_capacity_bounds_every_destination():
     """Per destination: the most touched rows any batch has on one owner (row r -> r % W) plus
     the negatives' expected share with slack; even (16-byte aligned rows)."""

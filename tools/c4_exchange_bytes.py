@@ -29,14 +29,14 @@ def main():
     train = synth.train_split(g.edge_index, 0.9, seed=0)
     _, f_intra, lists = cluster.cluster_batches(train, g.num_nodes, 1024, 32)
     batches = [_B(torch.from_numpy(x)) for x in lists]
-    U, N = g.num_users, g.num_nodes
+    U, I, N = g.num_users, g.num_items, g.num_nodes
     cap = D.exchange_capacity(batches, U)
     cap += cap % 2
     rep_blk = cap * (d + 2) * 4
     print(f"C3 batches: {len(batches)}, f_intra {f_intra:.4f}, replicated slots per rank {cap} "
           f"({rep_blk / 1e6:.2f} MB record block)")
     for W in (2, 4, 8):
-        ocap = owner_capacity(batches, U, W)
+        ocap = owner_capacity(batches, U, W, num_items=I)
         blk = ocap * (d + 2) + 2 * ocap
         blk += (-blk) % 4
         steps_per_epoch = len(batches) // W

@@ -156,7 +156,7 @@ def main():
         # T_1 carries one flush per 32 steps; a W-rank epoch is 32 / W steps
         extra_flush = flush * (1.0 / (len(batches) // W) - 1.0 / len(batches))
         spe = len(batches) // W  # steps per epoch (each step takes W batches)
-        ocap = owner_capacity(batches, U, W)
+        ocap = owner_capacity(batches, U, W, num_items=I)
         oblk = ocap * (d + 2) + 2 * ocap
         oblk += (-oblk) % 4
         owned_rows = -(-N // W)
