@@ -501,7 +501,7 @@ def main():
                     help="train, N=1: run the row exchange anyway (measures its kernels; N>1 always uses it)")
     ap.add_argument("--dp-lr", choices=["sqrt", "same"], default="sqrt",
                     help="train, data parallel: Adam lr 1e-3 * sqrt(W) (default; lgcn_amd.distributed.dp_lr) or 1e-3")
-    ap.add_argument("--dp-mode", choices=["auto", "replicated", "owner", "columns"], default="auto",
+    ap.add_argument("--dp-mode", choices=["auto", "replicated", "owner", "columns", "hybrid"], default="auto",
                     help="train, N > 1: column-sharded exact training (every rank the same batches on d/N "
                          "columns, one [B, 6] all_reduce per step — the one-GPU step's semantics, so Recall is "
                          "the one-GPU run's), or data parallel over disjoint parts with a replicated row-lazy "
@@ -987,12 +987,15 @@ def run_train(args):
     lazy = not (args.autograd or args.torch_adam or args.dense_adam)
     dp_mode = args.dp_mode if world > 1 else "replicated"
     if dp_mode == "auto":
-        # tools/project_c4.py on the C3 batches (profiles/r05g_c4proj/): at W = 2 no mode beats one GPU
-        # by much and columns keeps the one-GPU semantics; from W = 4 the owner-sharded exchange is
-        # the fastest (W = 8: 1.9x at 100 GB/s, 2.7x at 200, against ~1.0x for columns)
-        dp_mode = "columns" if world <= 2 else "owner"
+        # tools/project_c4.py (profiles/r05zp_hybrid/): at W = 2 no mode beats one GPU by much and
+        # columns keeps the one-GPU semantics; from W = 4, on batches that draw fewer negatives than
+        # there are items (C3: 10k triplets, 59k items) the owner-sharded exchange is the fastest
+        # (W = 8: 1.8x at 100 GB/s, 2.6x at 200), on batches whose negatives cover the items (the
+        # planted graph: 180k triplets) the hybrid one (2.8x / 3.9x, owner 2.3x / 3.2x)
+        mean_b = float(np.mean([int((b.edge_index[0] < U).sum()) for b in batches]))
+        dp_mode = "columns" if world <= 2 else ("hybrid" if mean_b >= I else "owner")
     if dp_mode != "replicated" and not lazy:
-        raise SystemExit("--dp-mode owner / columns need the row-lazy Adam (no --autograd/--torch-adam/--dense-adam)")
+        raise SystemExit("--dp-mode owner / columns / hybrid need the row-lazy Adam (no --autograd/--torch-adam/--dense-adam)")
     cols = None
     if dp_mode == "columns":
         from lgcn_amd.train_step import ColumnGroup
@@ -1033,6 +1036,11 @@ def run_train(args):
                                  _ffi.load().lgcn_row_grad_norm_workspace_floats())
         log(f"[rank {rank}] owner exchange: {exchange.cap} slots per destination, blocks of "
             f"{exchange.blk * 4 / 1e6:.2f} MB, two all_to_alls per step")
+    elif dp_mode == "hybrid":
+        # items all_reduced densely, users' rows as record blocks (large batches)
+        exchange = D.HybridExchange(D.user_exchange_capacity(batches, U), U, opt.gi, dev, world)
+        log(f"[rank {rank}] hybrid exchange: {exchange.cap} user slots per rank ({exchange.blk * 4 / 1e6:.2f} MB "
+            f"record block) + the item gradient table ({I * d * 4 / 1e6:.1f} MB) all_reduced per step")
     elif dp_mode == "replicated" and lazy and (world > 1 or args.exchange):
         # row-sparse DP gradient exchange: all_gather of each rank's nonzero gradient rows
         cap = D.exchange_capacity(batches, U)
@@ -1132,6 +1140,8 @@ def run_train(args):
                                    ("owner-sharded row-lazy Adam (row r owned by rank r % W): gradient rows to their "
                                     "owners and the next step's rows back, two all_to_alls + the clip norm's "
                                     "partials per step" if dp_mode == "owner" else
+                                    "item gradient table all_reduced densely, users' rows all-gathered as records, "
+                                    "every item row and the users' union stepped" if dp_mode == "hybrid" else
                                     "row-sparse gradient exchange (one all_gather per step of each rank's nonzero rows and their ids), "
                                     "row-lazy Adam on the union" if exchange is not None else
                                     "RCCL all_reduce of embedding grads" if world > 1 else "single GPU"))},

@@ -146,6 +146,53 @@ class RowExchange:
             dist.all_gather(list(self.pack_all.view(self.world, self.blk).unbind(0)), self.pack)
 
 
+def user_exchange_capacity(batches, num_users: int) -> int:
+    """Slots per rank for HybridExchange's user records: the most user rows any batch touches,
+    agreed across ranks."""
+    cap = 0
+    for b in batches:
+        cap = max(cap, int((torch.unique(b.edge_index) < num_users).sum()))
+    world, _ = world_info()
+    if world > 1:
+        t = torch.tensor([cap], dtype=torch.int64)
+        if device_collectives():
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        cap = int(t.item())
+    return cap
+
+
+class HybridExchange(RowExchange):
+    """Data-parallel exchange for LARGE batches (a structured graph's Cluster-GCN batches, where a
+    step's B negatives cover nearly every item): the item gradient table is all_reduced densely —
+    I x d floats, less than the sparse records of ~I distinct item rows plus their ids — and only
+    the users' rows (each user is in one part, so one rank's batch, per epoch) travel as
+    RowExchange record blocks. Every rank then steps the union of the users' rows and ALL item
+    rows (an item without a gradient this step takes Adam's zero-gradient step, bitwise what the
+    row-lazy replay would give it later). The item sums are the collective's (RCCL ring / gloo), not
+    rank order: at W = 2 bitwise the replicated exchange (a + b == b + a), above it equal to
+    rounding; every rank's tables stay bitwise identical (every rank receives the same sums).
+
+    gi: the optimizer's item gradient table (RowLazyAdam.gi), zeroed by the step before it writes
+    and summed in place."""
+
+    dense_items = True
+
+    def __init__(self, cap_users: int, num_users: int, gi: torch.Tensor, device, world: int):
+        I, d = gi.shape
+        super().__init__(cap_users, int(num_users) + int(I), d, device, world)
+        self.U = int(num_users)
+        self.gi = gi
+        self.items_all = torch.arange(self.U, self.U + int(I), dtype=torch.int32, device=device)
+
+    def gather(self) -> None:
+        super().gather()  # the users' record blocks
+        if self.world == 1:
+            return
+        self.bytes += int(2 * (self.world - 1) * self.gi.numel() * 4 // self.world)  # ring all_reduce
+        dist.all_reduce(self.gi, op=dist.ReduceOp.SUM)
+
+
 def train_epoch(model, optimizer, batches, device, seed: int = 0, epoch: int = 0, loss_fn=None,
                 embed_fn=None, max_norm: float = 1.0) -> float:
     """One data-parallel epoch; returns the global edge-weighted mean loss (as reference train())."""

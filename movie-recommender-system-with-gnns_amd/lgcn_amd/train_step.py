@@ -193,6 +193,8 @@ class _BatchState:
             self.fixed_dense, self.fixed_sparse, self.fixed_touched = segment_directions(
                 self.keys[:2 * B], N, chunk=batch_chunk_for(2 * B), row_mask=self.plan.touched)
             self.touched_rows = torch.nonzero(self.plan.touched).squeeze(1).to(torch.int32).contiguous()
+            # ascending: the user rows first (HybridExchange packs only those)
+            self.touched_users = self.touched_rows[:int((self.touched_rows < U).sum())]
         elif self.small:
             self.fixed_dense, self.fixed_sparse = segment_directions(self.keys[:2 * B], N, chunk=batch_chunk_for(2 * B))
         if self.small and B >= sorted_scatter_min_b():
@@ -338,8 +340,9 @@ class FusedTrainStep:
         per-batch hipGraph and replayed from then on; negatives still come from the global CUDA
         generator (graph-safe Philox offsets), so each replay draws new ones.
         exchange (lazy, data parallel): a lgcn_amd.distributed.RowExchange (replicated optimizer;
-        the step is two captured halves around the eager all_gather of the packed gradient rows) or
-        a lgcn_amd.owner.OwnerExchange (owner-sharded optimizer: step(batch, next_batch) — the
+        the step is two captured halves around the eager all_gather of the packed gradient rows), a
+        lgcn_amd.distributed.HybridExchange (the same, the item gradient table all_reduced whole:
+        large batches) or a lgcn_amd.owner.OwnerExchange (owner-sharded optimizer: step(batch, next_batch) — the
         rows of next_batch's step are fetched from their owners at the end of this one).
         neg_seed: draw step k's negatives from a generator seeded (neg_seed, k) instead of the
         global CUDA generator (the same draws whichever exchange runs, and whenever they are drawn).
@@ -380,6 +383,7 @@ class FusedTrainStep:
             if model.dim_h != cols.d:
                 raise ValueError(f"the model holds {model.dim_h} columns, the ColumnGroup share is {cols.d}")
         self.owner = isinstance(exchange, OwnerExchange)
+        self.hybrid = getattr(exchange, "dense_items", False)
         if self.owner and not lazy:
             raise ValueError("an OwnerExchange needs lazy=True (RowLazyAdam)")
         self.neg_seed = neg_seed
@@ -548,6 +552,8 @@ class FusedTrainStep:
             out = propagate_forward(uw.detach(), iw.detach(), st.plan, K)
             reg_coeff = self._bpr(lib, st, out, uw, iw, U, N, B, d, div, mul, stream)
             gu, gi = opt.gu, opt.gi
+            if self.hybrid:  # the whole item table is all_reduced: rows this step leaves alone are 0
+                gi.zero_()
             grads = (gu, gi, U)
             # seed g = (dF * mul) / div on every touched row (0 where no (user, positive) key)...
             spmm(st.fixed_touched, N, d, (st.cf, None, big), None, grads, None, _ffi.EPI_SCALE, div, mul,
@@ -568,6 +574,11 @@ class FusedTrainStep:
                                                     st.c2flag.data_ptr(), st.plan.touched.data_ptr(), ex.world,
                                                     ex.cap, ex.blk, ex.counts.data_ptr(), ex.send.data_ptr(),
                                                     ex.overflow.data_ptr(), stream), "lgcn_owner_pack_rows")
+            elif self.hybrid:
+                # the users' rows -> the record slots (the item table goes whole, all_reduced)
+                _ffi.check(lib.lgcn_rows_pack(gu.data_ptr(), gi.data_ptr(), U, d, st.touched_users.data_ptr(),
+                                              st.touched_users.numel(), None, 0, U, None, None, ex.cap,
+                                              ex.ids.data_ptr(), ex.rows.data_ptr(), stream), "lgcn_rows_pack(users)")
             elif ex is not None:
                 # this rank's rows with a possibly nonzero gradient -> the exchange slots
                 _ffi.check(lib.lgcn_rows_pack(gu.data_ptr(), gi.data_ptr(), U, d, st.touched_rows.data_ptr(),
@@ -599,6 +610,12 @@ class FusedTrainStep:
                                                 ex.first.data_ptr(), opt.gu.data_ptr(), opt.gi.data_ptr(),
                                                 m.num_users, m.dim_h, float(ex.world), stream),
                        "lgcn_rows_accumulate")
+            if self.hybrid:
+                # the all_reduced item sums / W (as lgcn_rows_accumulate divides), then every item row
+                # and the union of the users' rows
+                opt.gi.div_(float(ex.world))
+                opt.step_rows(ex.items_all, ex.ids_all, 0, first_b=ex.first)
+                return
             opt.step_rows(None, ex.ids_all, 0, first_b=ex.first)
 
     # --- owner-sharded exchange (lgcn_amd.owner) ----------------------------------------------

@@ -1,7 +1,8 @@
 """One rank of the data-parallel training check in tests/test_gpu_exchange.py (started as a
 child process per rank; gloo over one GPU): trains the same Cluster-GCN batches several ways —
 dense FusedAdam after an all_reduce of both gradients, the row-lazy Adam with the row-sparse
-exchange or the owner-sharded exchange, and column-sharded (DP_VARIANTS cols / cols_graphs), each
+exchange, the owner-sharded exchange or the hybrid one (DP_VARIANTS hybrid / hybrid_graphs: items
+all_reduced densely), and column-sharded (DP_VARIANTS cols / cols_graphs), each
 eager and hipGraph-replayed — and saves the final tables and losses.
 
 python tests/dp_exchange_worker.py RANK WORLD PORT OUT CLIP [BATCHES.npz]
@@ -87,6 +88,8 @@ def main():
                               max_grad_norm=clip_)
             if name.startswith("owner"):
                 ex = OwnerExchange(ocap, U + I, d, gpu, world, rank, _ffi.load().lgcn_row_grad_norm_workspace_floats())
+            elif name.startswith("hybrid"):
+                ex = D.HybridExchange(D.user_exchange_capacity(batches, U), U, opt.gi, gpu, world)
             else:
                 ex = D.RowExchange(cap, U + I, d, gpu, world)
             step = FusedTrainStep(m, opt, world=world, lazy=True, exchange=ex, graphs=name.endswith("_graphs"),

@@ -15,7 +15,9 @@ the column split (W = 1).
 
 LR_SCALE (dp only, default 1): the data-parallel Adam's lr is 1e-3 * LR_SCALE (tools/dp_lr_probe.py).
 
-python tests/dp_recall_worker.py RANK WORLD PORT OUT EPOCHS PARTS [MODE: dp | cols | plain] [LR_SCALE]"""
+MODE "hybrid": data parallel with lgcn_amd.distributed.HybridExchange (items all_reduced densely).
+
+python tests/dp_recall_worker.py RANK WORLD PORT OUT EPOCHS PARTS [MODE: dp | hybrid | cols | plain] [LR_SCALE]"""
 import json
 import os
 import sys
@@ -80,7 +82,7 @@ def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
     epochs, parts = int(sys.argv[5]), int(sys.argv[6])
     mode = sys.argv[7] if len(sys.argv) > 7 else "dp"
-    lr_scale = float(sys.argv[8]) if len(sys.argv) > 8 and mode == "dp" else 1.0
+    lr_scale = float(sys.argv[8]) if len(sys.argv) > 8 and mode in ("dp", "hybrid") else 1.0
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -115,15 +117,18 @@ def main():
     if mode == "dp":
         ex = D.RowExchange(D.exchange_capacity(batches, U), U + I, 64, gpu, world) if world > 1 else None
         step = FusedTrainStep(m, opt, world=world, lazy=True, exchange=ex, neg_seed=1000 + rank)
+    elif mode == "hybrid":  # data parallel, the item gradient table all_reduced densely
+        ex = D.HybridExchange(D.user_exchange_capacity(batches, U), U, opt.gi, gpu, world)
+        step = FusedTrainStep(m, opt, world=world, lazy=True, exchange=ex, neg_seed=1000 + rank)
     else:  # the reference's schedule on every rank, the same negatives everywhere
         step = FusedTrainStep(m, opt, lazy=True, cols=cg, neg_seed=7)
     steps, losses, first_tables, first_grads = 0, [], None, None
     for epoch in range(epochs):
-        sched_world, sched_rank = (world, rank) if mode == "dp" else (1, 0)
+        sched_world, sched_rank = (world, rank) if mode in ("dp", "hybrid") else (1, 0)
         for i, b in enumerate(D.rank_share(len(batches), sched_world, sched_rank, seed=0, epoch=epoch)):
             losses.append(float(step.step(batches[b]).item()))
             steps += 1
-            if steps == 1 and mode != "dp":
+            if steps == 1 and mode not in ("dp", "hybrid"):
                 step.sync()
                 first_tables = gather_columns(m, cg, world)
                 # the first step's gradient rows (touched rows + first-occurrence negatives outside them)
@@ -135,8 +140,8 @@ def main():
                 first_grads = (ids.cpu(), gather_tensor_columns(g, cg, world))
         step.sync()
     torch.cuda.synchronize()
-    full = gather_columns(m, cg, world) if mode != "dp" else None
-    if rank == 0 and mode != "dp":
+    full = gather_columns(m, cg, world) if mode not in ("dp", "hybrid") else None
+    if rank == 0 and mode not in ("dp", "hybrid"):
         torch.save({"losses": losses, "first": first_tables, "first_grads": first_grads, "final": full}, out + ".pt")
     if rank == 0:
         if full is not None:  # score the gathered full-width tables

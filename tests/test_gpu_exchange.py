@@ -281,6 +281,38 @@ def test_dp8_owner_exchange_dense_batches_matches_replicated(gpu, tmp_path):
           f"replicated {res[0]['lazy']['bytes_per_step'] / 1e6:.3f} MB, owner {res[0]['owner']['bytes_per_step'] / 1e6:.3f} MB")
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_hybrid_exchange_matches_replicated(gpu, tmp_path, world):
+    """HybridExchange (item gradient table all_reduced densely, users' rows as record blocks,
+    every item row stepped each step): every rank ends bitwise identical, eager == graphs; at W = 2
+    bitwise the replicated row exchange (a + b == b + a; the item rows a step leaves alone take
+    Adam's zero-gradient step, bitwise the lazy replay); at W = 4 the item sums are the
+    collective's order, not rank order — losses to 1e-5 of the replicated run's, tables within
+    Adam's reach (2 lr per step) with all but 1e-3 of the elements inside the 1e-5 row bar."""
+    res = _spawn(world, tmp_path, float("inf"), "lazy,hybrid,hybrid_graphs", steps=12)
+    for name in ("lazy", "hybrid", "hybrid_graphs"):
+        for r in range(1, world):
+            assert torch.equal(res[0][name]["user"], res[r][name]["user"]), (name, r)
+            assert torch.equal(res[0][name]["item"], res[r][name]["item"]), (name, r)
+    lz, hy, hg = res[0]["lazy"], res[0]["hybrid"], res[0]["hybrid_graphs"]
+    assert hy["losses"] == hg["losses"]
+    assert torch.equal(hy["user"], hg["user"]) and torch.equal(hy["item"], hg["item"])
+    if world == 2:
+        assert hy["losses"] == lz["losses"]
+        assert torch.equal(hy["user"], lz["user"]) and torch.equal(hy["item"], lz["item"])
+        return
+    for a, b in zip(lz["losses"], hy["losses"]):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(a))
+    for k in ("user", "item"):
+        x, y = lz[k], hy[k]
+        assert (x - y).abs().max().item() <= 2 * 1e-2 * 12
+        scale = x.abs().amax(dim=1, keepdim=True).clamp_min(1e-30)
+        off = ((x - y).abs() > 1e-5 * scale).float().mean().item()
+        assert off <= 1e-3, (k, off)
+    print(f"W={world} hybrid vs replicated: bytes received per rank per step {hy['bytes_per_step'] / 1e6:.3f} MB "
+          f"vs {lz['bytes_per_step'] / 1e6:.3f} MB")
+
+
 @pytest.mark.parametrize("world,clip", [(2, float("inf")), (2, 1.0), (4, 1.0)])
 def test_column_sharded_graph_replay_matches_eager(gpu, tmp_path, world, clip):
     """Column-sharded training captured per batch as graphs cut at its two collectives

@@ -12,6 +12,9 @@ priced from a bus bandwidth and a latency per collective, which a one-GPU box ca
               Adam on the UNION of the W batches' rows (timed by emulation: the W ranks' blocks
               computed one after another on this GPU, then the union update timed alone) + the
               per-epoch flush (32 / W steps per epoch). Weak: speed-up = W T_1(d) / step_W.
+  hybrid      the replicated step with the item gradient table all_reduced densely (ring) and only
+              the users' rows all-gathered; every item row stepped each step (update timed by
+              emulation with W ranks' user blocks). Weak.
   owner       the replicated step with the union update shared by the W owners (each owner
               updates 1/W of the union: the replicated union update / W, a lower bound) and two
               all_to_alls of (W-1)/W of its blocks instead of the all_gather, plus the per-epoch
@@ -44,7 +47,9 @@ def _ev():
 def one_gpu_step_ms(U, I, d, batches, exchange=False, epochs=3):
     """ms per step of the fused lazy step over whole epochs of the batches (graphs, flush once per
     epoch inside the timed region) at width d, the bench's C3 loop; with exchange=True the W = 1
-    row exchange runs too (its pack / mark / accumulate kernels)."""
+    row exchange runs too (its pack / mark / accumulate kernels); exchange="hybrid": the W = 1
+    HybridExchange (the item gradient table zeroed each step, the users packed, every item row
+    stepped)."""
     from lgcn_amd import distributed as D
     from lgcn_amd.optim import RowLazyAdam
     from lgcn_amd.train_step import FusedTrainStep
@@ -55,7 +60,10 @@ def one_gpu_step_ms(U, I, d, batches, exchange=False, epochs=3):
     m = LightGCN(U, I, num_layers=3, dim_h=d).to(dev)
     opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-3, max_grad_norm=1,
                       max_steps=4096)
-    ex = D.RowExchange(D.exchange_capacity(batches, U), U + I, d, dev, 1) if exchange else None
+    if exchange == "hybrid":
+        ex = D.HybridExchange(D.user_exchange_capacity(batches, U), U, opt.gi, dev, 1)
+    else:
+        ex = D.RowExchange(D.exchange_capacity(batches, U), U + I, d, dev, 1) if exchange else None
     step = FusedTrainStep(m, opt, graphs=True, lazy=True, exchange=ex)
     for _ in range(2):  # warm-up epochs: plans built, graphs captured
         for b in batches:
@@ -119,6 +127,44 @@ def union_update_ms(U, I, d, batches, W, reps=6):
     return float(np.median(ts)), ex.blk * 4, a.elapsed_time(z)
 
 
+def hybrid_update_ms(U, I, d, batches, W, reps=6):
+    """HybridExchange's update on W ranks' user records (emulated as union_update_ms does) plus
+    every item row: mark first + the users' rank-order sums + the item table / W + clip norm + row
+    Adam on all items and the union of the users."""
+    from lgcn_amd import distributed as D
+    from lgcn_amd.optim import RowLazyAdam
+    from lgcn_amd.train_step import FusedTrainStep
+    from models.light_gcn import LightGCN
+
+    torch.manual_seed(0)
+    dev = batches[0].edge_index.device
+    m = LightGCN(U, I, num_layers=3, dim_h=d).to(dev)
+    opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-3, max_grad_norm=1,
+                      max_steps=4096)
+    ex = D.HybridExchange(D.user_exchange_capacity(batches, U), U, opt.gi, dev, W)
+    step = FusedTrainStep(m, opt, world=W, graphs=False, lazy=True, exchange=ex)
+    order = np.random.default_rng(0).permutation(len(batches))
+    ts = []
+    k = 0
+    for rep in range(reps + 2):
+        group = [batches[order[(k + r) % len(batches)]] for r in range(W)]
+        k += W
+        with torch.no_grad():
+            for r, b in enumerate(group):
+                st = step.state(b.edge_index)
+                step._lazy_grads(st)
+                ex.pack_all.view(W, ex.blk)[r].copy_(ex.pack)
+        torch.cuda.synchronize()
+        a, z = _ev(), _ev()
+        a.record()
+        step._lazy_update(st)
+        z.record()
+        torch.cuda.synchronize()
+        if rep >= 2:
+            ts.append(a.elapsed_time(z))
+    return float(np.median(ts)), ex.blk * 4
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--graph", choices=["ml25m", "planted"], default="ml25m")
@@ -144,15 +190,18 @@ def main():
     t1 = one_gpu_step_ms(U, I, d, batches)
     t1x = one_gpu_step_ms(U, I, d, batches, exchange=True)
     upd1, _, flush = union_update_ms(U, I, d, batches, 1)
+    t1h = one_gpu_step_ms(U, I, d, batches, exchange="hybrid")
+    upd1h, _ = hybrid_update_ms(U, I, d, batches, 1)
     print(f"C4 projection, {args.graph} graph: {len(batches)} batches of {E_mean:.0f} edges (B {B_mean:.0f} "
           f"triplets), f_intra {f_intra:.4f}, K=3 d={d}. One GPU: {t1:.4f} ms per step ({3 * E_mean / t1 / 1e6:.3g}e9 "
-          f"edges/s); with the W=1 row exchange {t1x:.4f} ms; own-rows update {upd1 * 1e3:.1f} us; per-epoch "
-          f"flush {flush * 1e3:.1f} us", flush=True)
+          f"edges/s); with the W=1 row exchange {t1x:.4f} ms, with the W=1 hybrid exchange {t1h:.4f} ms; own-rows "
+          f"update {upd1 * 1e3:.1f} us (hybrid {upd1h * 1e3:.1f}); per-epoch flush {flush * 1e3:.1f} us", flush=True)
     for W in worlds:
         if d % W or (d // W) % 4:
             continue
         tc = one_gpu_step_ms(U, I, d // W, batches)
         updW, blk_bytes, _ = union_update_ms(U, I, d, batches, W)
+        updWh, hblk_bytes = hybrid_update_ms(U, I, d, batches, W)
         # T_1 carries one flush per 32 steps; a W-rank epoch is 32 / W steps
         extra_flush = flush * (1.0 / (len(batches) // W) - 1.0 / len(batches))
         spe = len(batches) // W  # steps per epoch (each step takes W batches)
@@ -161,8 +210,9 @@ def main():
         oblk += (-oblk) % 4
         owned_rows = -(-N // W)
         print(f" W={W}: columns rank step (d={d // W}) {tc:.4f} ms; union update {updW * 1e3:.1f} us "
-              f"(own rows {upd1 * 1e3:.1f}); record block {blk_bytes / 1e6:.2f} MB, owner block {oblk * 4 / 1e6:.2f} MB",
-              flush=True)
+              f"(own rows {upd1 * 1e3:.1f}); hybrid update {updWh * 1e3:.1f} us (own {upd1h * 1e3:.1f}); record "
+              f"block {blk_bytes / 1e6:.2f} MB, owner block {oblk * 4 / 1e6:.2f} MB, hybrid user block "
+              f"{hblk_bytes / 1e6:.2f} MB + items {I * d * 4 / 1e6:.1f} MB all_reduced", flush=True)
         for bw in (float(v) for v in args.busbw.split(",")):
             # columns: all_reduce of [B, 6] floats + all_gather of W x 2048 norm partials
             cols = tc + 2 * lat + (2 * (W - 1) / W * B_mean * 24 + (W - 1) * 2048 * 4) / 1e6 / bw
@@ -172,9 +222,13 @@ def main():
             # the per-epoch all_gather of the owned rows spread over the epoch's steps
             own = (t1x + 3 * lat + (2 * (W - 1) * oblk * 4 + (W - 1) * 2048 * 4) / 1e6 / bw + (updW / W - upd1 / W)
                    + (lat + (W - 1) * owned_rows * d * 4 / 1e6 / bw) / spe)
+            # hybrid: own step (zeroed item table, users packed, all items stepped) + the users' all_gather
+            # + a ring all_reduce of the item gradient table + the union update's extra over the own one
+            hyb = (t1h + 2 * lat + ((W - 1) * hblk_bytes + 2 * (W - 1) / W * I * d * 4) / 1e6 / bw
+                   + (updWh - upd1h) + extra_flush)
             print(f"   busbw {bw:.0f} GB/s (+{args.lat_us:.0f} us each): columns {cols:.4f} ms ({t1 / cols:.2f}x) | "
-                  f"replicated {rep:.4f} ms ({W * t1 / rep:.2f}x) | owner {own:.4f} ms ({W * t1 / own:.2f}x)",
-                  flush=True)
+                  f"replicated {rep:.4f} ms ({W * t1 / rep:.2f}x) | owner {own:.4f} ms ({W * t1 / own:.2f}x) | "
+                  f"hybrid {hyb:.4f} ms ({W * t1 / hyb:.2f}x)", flush=True)
 
 
 if __name__ == "__main__":
