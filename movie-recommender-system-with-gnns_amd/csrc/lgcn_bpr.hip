@@ -15,6 +15,8 @@
 //                 sorted) order using the CSR lgcn_csr_build makes of the 3B row keys.
 // The gradient is the analytic derivative of the same expression (not bitwise torch autograd).
 
+#include <climits>
+
 #include "lgcn_common.h"
 
 using namespace lgcn;
@@ -364,6 +366,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_rows(const int64_t* __restri
 constexpr int kRangeCap = 4096;
 
 constexpr int kRSBlock = 1024;          // 16 waves: more lane groups for the per-row sums
+constexpr int kRSSpanTable = 2048;      // spans up to this many rows keep per-row tables in LDS
 constexpr int kRSWaves = kRSBlock / 64;
 constexpr int kRSChunks = 4;            // 64-key chunks per wave per round (coalesced)
 
@@ -387,6 +390,12 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
     __shared__ int lidx[kRangeCap];
     __shared__ int wave_cnt[kRSWaves];
     __shared__ int list_n;
+    // per row of the span (span <= kRSSpanTable): its first list entry and its entry count, so an
+    // entry knows whether it is its row's first and, for the common single-occurrence row, needs
+    // no scan of the list (the scans were the launch's critical path: profiles/r05zv_range_scatter/)
+    __shared__ int lfirst[kRSSpanTable];
+    __shared__ int lcount[kRSSpanTable];
+    const bool tables = span <= kRSSpanTable;
     const int64_t lo = int64_t(blockIdx.x) * span;
     const int64_t hi = lo + span < nrows ? lo + span : nrows;
     const int lane = threadIdx.x & 63;
@@ -461,14 +470,30 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
         }
         // sum every row of the list in list order
         const int n = list_n;
+        if (tables) {
+            for (int i = threadIdx.x; i < span; i += kRSBlock) {
+                lfirst[i] = INT_MAX;
+                lcount[i] = 0;
+            }
+            __syncthreads();
+            for (int e = threadIdx.x; e < n; e += kRSBlock) {
+                atomicMin(&lfirst[lkey[e]], e);
+                atomicAdd(&lcount[lkey[e]], 1);
+            }
+            __syncthreads();
+        }
         for (int e = g; e < n; e += GPB) {
             const int key = lkey[e];
             bool first = true;
-            for (int q = 0; q < e; ++q)
-                if (lkey[q] == key) {
-                    first = false;
-                    break;
-                }
+            if (tables) {
+                first = lfirst[key] == e;
+            } else {
+                for (int q = 0; q < e; ++q)
+                    if (lkey[q] == key) {
+                        first = false;
+                        break;
+                    }
+            }
             // every b is in exactly one list: its flag is written here (1 = the row's parked C2 sum)
             if (second && l == 0) c2flag[lidx[e]] = first ? 1 : 0;
             if (!first) continue;
@@ -479,7 +504,9 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                 acc2[k] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
             int64_t occ = 0;
-            for (int q = e; q < n; ++q) {
+            // a row with one entry sums just it; else the entries from e on, in list order
+            const int q_end = (tables && lcount[key] == 1) ? e + 1 : n;
+            for (int q = e; q < q_end; ++q) {
                 if (lkey[q] != key) continue;
                 ++occ;
                 const float4* c = reinterpret_cast<const float4*>(C + int64_t(lidx[q]) * d) + l;
