@@ -104,3 +104,44 @@ def test_single_rank_equals_reference_train():
         res.append((loss, m.user_embedding.weight.detach().clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1])
+
+
+def _hybrid_worker(rank, world, port, out_dir):
+    import sys
+
+    from conftest import PKG, ROOT
+    sys.path[:0] = [str(PKG), str(ROOT)]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    U, I, batches = _batches()
+    cap = D.user_exchange_capacity(batches, U)
+    gi = torch.full((I, 4), float(rank + 1))  # rank r's item gradient table: r + 1 everywhere
+    ex = D.HybridExchange(cap, U, gi, torch.device("cpu"), world)
+    ex.ids.fill_(-1)
+    ex.ids[:2] = torch.tensor([rank, U - 1 - rank])  # two user records per rank
+    ex.rows[:2] = float(10 * (rank + 1))
+    ex.gather()
+    np.save(os.path.join(out_dir, f"h{rank}.npy"), np.concatenate([
+        np.array([cap, ex.bytes], dtype=np.float64), gi.numpy().ravel().astype(np.float64),
+        ex.pack_all.view(world, ex.blk)[:, :2 * ex.cap].contiguous().view(torch.int64)[:, :2].numpy().ravel()
+        .astype(np.float64)]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_hybrid_exchange_gathers_users_and_sums_items(tmp_path):
+    """HybridExchange (lgcn_amd.distributed) over gloo, world 2: the users' record blocks are
+    all-gathered in rank order, the item gradient table is summed in place on every rank, and the
+    capacity is the most user rows any batch touches."""
+    port = _free_port()
+    mp.spawn(_hybrid_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    U, I, batches = _batches()
+    want_cap = max(int((torch.unique(b.edge_index) < U).sum()) for b in batches)
+    h0, h1 = np.load(tmp_path / "h0.npy"), np.load(tmp_path / "h1.npy")
+    assert np.array_equal(h0, h1)  # every rank: the same capacity, bytes, sums and gathered ids
+    assert int(h0[0]) == want_cap
+    items = h0[2:2 + I * 4]
+    assert np.all(items == 3.0)  # 1 + 2 on both ranks
+    ids = h0[2 + I * 4:].reshape(2, 2)
+    assert ids.tolist() == [[0, U - 1], [1, U - 2]]  # rank order
