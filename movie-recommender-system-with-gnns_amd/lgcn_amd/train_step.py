@@ -342,8 +342,9 @@ class FusedTrainStep:
         exchange (lazy, data parallel): a lgcn_amd.distributed.RowExchange (replicated optimizer;
         the step is two captured halves around the eager all_gather of the packed gradient rows), a
         lgcn_amd.distributed.HybridExchange (the same, the item gradient table all_reduced whole:
-        large batches) or a lgcn_amd.owner.OwnerExchange (owner-sharded optimizer: step(batch, next_batch) — the
-        rows of next_batch's step are fetched from their owners at the end of this one).
+        large batches) or a lgcn_amd.owner.OwnerExchange (owner-sharded optimizer:
+        step(batch, next_batch) — the rows of next_batch's step are fetched from their owners at
+        the end of this one).
         neg_seed: draw step k's negatives from a generator seeded (neg_seed, k) instead of the
         global CUDA generator (the same draws whichever exchange runs, and whenever they are drawn).
         cols (lazy): column-sharded training — the model holds this rank's ColumnGroup columns,
