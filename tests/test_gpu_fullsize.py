@@ -35,6 +35,34 @@ def test_c2_full_forward_matches_oracle(gpu, c2):
     assert_rows_close(out, ref)
 
 
+@pytest.mark.parametrize("d", [8, 16, 32])
+def test_c2_column_share_widths_match_oracle(gpu, c2, d):
+    """The narrow widths the 1 x F column grids run at C2 size (d = 64 / F), through their default
+    source-sliced schedules (4 / 8 / 12 MB slices: lgcn_amd.plan.slice_bytes_for): the K=3 forward
+    per row within 1e-5 of the C oracle, and one layer bitwise on every unsplit row."""
+    from lgcn_amd import propagate_forward
+    from lgcn_amd.plan import slice_bytes_for
+    from lgcn_amd.propagate import lgconv_forward
+
+    g, plan = c2
+    assert slice_bytes_for(g.num_nodes, d) > 0
+    sched = plan.schedule("fwd", d)
+    assert hasattr(sched, "launches")  # the sliced schedule, not the plain one
+    rng = np.random.default_rng(d)
+    uw = (rng.standard_normal((g.num_users, d)) * 0.01).astype(np.float32)
+    iw = (rng.standard_normal((g.num_items, d)) * 0.01).astype(np.float32)
+    out = propagate_forward(torch.from_numpy(uw).to(gpu), torch.from_numpy(iw).to(gpu), plan, 3).cpu().numpy()
+    ru, ri = c_oracle.lightgcn_forward(uw, iw, g.edge_index, 3)
+    assert_rows_close(out, np.concatenate([ru, ri]))
+    x = np.concatenate([uw, iw])
+    y = lgconv_forward(torch.from_numpy(x).to(gpu), plan).cpu().numpy()
+    _, w = c_oracle.gcn_norm(g.edge_index, g.num_nodes)
+    ref = c_oracle.lgconv(x, g.edge_index, w)
+    mask = np.ones(g.num_nodes, bool)
+    mask[sched.splits[: sched.n_splits, 0].cpu().numpy()] = False
+    assert np.array_equal(y[mask], ref[mask])
+
+
 def test_c2_single_layer_bitwise_on_unsplit_rows(gpu, c2):
     """One layer: every row summed as one sequential chain (not cut into chunks — with the
     source-sliced schedule, a chain that runs through several slice launches) is bitwise the
