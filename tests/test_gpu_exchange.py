@@ -281,7 +281,7 @@ def test_dp8_owner_exchange_dense_batches_matches_replicated(gpu, tmp_path):
           f"replicated {res[0]['lazy']['bytes_per_step'] / 1e6:.3f} MB, owner {res[0]['owner']['bytes_per_step'] / 1e6:.3f} MB")
 
 
-@pytest.mark.parametrize("world,clip", [(2, float("inf")), (4, float("inf")), (2, 1.0)])
+@pytest.mark.parametrize("world,clip", [(2, float("inf")), (4, float("inf")), (8, float("inf")), (2, 1.0)])
 def test_hybrid_exchange_matches_replicated(gpu, tmp_path, world, clip):
     """HybridExchange (item gradient table all_reduced densely, users' rows as record blocks,
     every item row stepped each step): every rank ends bitwise identical, eager == graphs; at W = 2
