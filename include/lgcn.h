@@ -38,7 +38,7 @@ extern "C" {
 
 typedef void* lgcn_stream_t; /* a hipStream_t; NULL = the null stream */
 
-#define LGCN_ABI_VERSION 8
+#define LGCN_ABI_VERSION 9
 
 #define LGCN_OK 0
 #define LGCN_E_ARG (-1)         /* bad size / null pointer / unsupported argument */
@@ -555,6 +555,15 @@ int lgcn_score_filter(const float* Qn, int64_t Qpad, int64_t Qvalid, const float
 int lgcn_select_topk(const uint32_t* list_key, const int32_t* list_idx, const int32_t* list_n, int32_t dense_n,
                      int32_t cap, int32_t k, int64_t P, int64_t Qpad, int64_t Qvalid, uint32_t* thr_out,
                      int32_t* hits_out, lgcn_stream_t stream);
+/* CPU torch.topk's tie rule (ABI 9; replaces torch.topk(scores, k) at reference
+ * utils/train_test.py:197 as the reference runs it on a CPU): hits_out[q] = positives (index < P)
+ * among the k slots ATen's CPU topk fills — std::partial_sort when k * 64 <= M (k <= 4096), else
+ * std::nth_element(k - 1), libstdc++'s algorithms reproduced step for step on the (key, index)
+ * sequence — so the set chosen among EQUAL scores is the CPU reference's, not the lowest indices.
+ * list_key/list_idx: lgcn_score_filter's dense rows (stride 1, cap >= M); both are overwritten
+ * (the nth_element path permutes them in place). Padding queries [Qvalid, Qpad) get 0. */
+int lgcn_select_topk_stl(uint32_t* list_key, int32_t* list_idx, int64_t cap, int64_t M, int32_t k, int64_t P,
+                         int64_t Qpad, int64_t Qvalid, int32_t* hits_out, lgcn_stream_t stream);
 
 /* Host-only (no GPU): `draws` consecutive numpy legacy np.random.choice(n, size, replace=False)
  * calls (reference utils/train_test.py:187) on the MT19937 state (key[624], *pos) of

@@ -197,10 +197,6 @@ __global__ __launch_bounds__(kBlock, score_filter_waves<D>()) void k_score_filte
         const float* brow = &cs[buf][i * ROWF + h * H];
         // B in groups of G float4 per LDS wait (G*4 MFMAs behind each wait)
         constexpr int G = (H / 4) >= 4 ? 4 : (H / 4);
-#ifdef LGCN_VARIANT_NO_MFMA
-        for (int r = 0; r < 16; ++r) acc[r] = brow[r] * a[r];
-        if (false)
-#endif
 #pragma unroll
         for (int v0 = 0; v0 < H / 4; v0 += G) {
             float4 bv[G];
@@ -215,13 +211,6 @@ __global__ __launch_bounds__(kBlock, score_filter_waves<D>()) void k_score_filte
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * v + 3], bv[g].w, acc, 0, 0, 0);
             }
         }
-#ifdef LGCN_VARIANT_NO_EPI
-        if (acc[0] == 12345.f && acc[15] == 54321.f) list_n[0] = 1;  // keep acc live; never true
-        if (nxt < nblk) land(buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
-        continue;
-#endif
         // epilogue: column = candidate j (this lane's), rows = queries; branch-free test, and
         // a wave-uniform branch only for the (rare) slots where some lane passes
         const int64_t j = cb * 32 + i;
@@ -351,6 +340,243 @@ __global__ __launch_bounds__(kSelBlock) void k_select_topk(const uint32_t* __res
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// CPU torch.topk's tie rule (lgcn_select_topk_stl). On CPU, the reference's torch.topk(scores, k)
+// (utils/train_test.py:197) runs ATen's topk_impl_loop (TopKImpl.h): the row as (value, index)
+// pairs, then std::partial_sort(k) when k * 64 <= M, else std::nth_element(k - 1), both with the
+// comparator (isnan(x) && !isnan(y)) || x > y — libstdc++ (GCC 11) instantiated inside libtorch.
+// Which of several EQUAL scores make the top k is therefore whatever those two algorithms leave
+// in the first k slots; with duplicated candidate rows (an item that is a positive of one edge and
+// a sampled negative of another scores identically) that decides hits. The kernels below run the
+// same libstdc++ algorithms, step for step, on the same (key, index) sequence (checked against
+// torch.topk on tie-heavy rows in tests/test_recall_stl.py's host model of these steps).
+// Keys compare as the floats do: -0 is mapped onto +0's key (equal as floats), NaN is highest.
+namespace stl {
+
+struct El {
+    uint32_t k;
+    int32_t i;
+};
+
+__device__ __forceinline__ uint32_t canon(uint32_t k) { return k == 0x7FFFFFFFu ? 0x80000000u : k; }
+__device__ __forceinline__ bool comp(const El& x, const El& y) { return x.k > y.k; }
+
+// (key, index) arrays in LDS or global memory (flat addresses)
+struct Arr {
+    uint32_t* k;
+    int32_t* i;
+    __device__ __forceinline__ El get(int64_t p) const { return El{k[p], i[p]}; }
+    __device__ __forceinline__ void set(int64_t p, const El& e) const {
+        k[p] = e.k;
+        i[p] = e.i;
+    }
+    __device__ __forceinline__ void swap(int64_t a, int64_t b) const {
+        const El x = get(a), y = get(b);
+        set(a, y);
+        set(b, x);
+    }
+};
+
+// std::__adjust_heap + std::__push_heap
+__device__ void adjust_heap(const Arr& a, int64_t first, int64_t hole, int64_t len, El value) {
+    const int64_t top = hole;
+    int64_t second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (comp(a.get(first + second), a.get(first + second - 1))) --second;
+        a.set(first + hole, a.get(first + second));
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        a.set(first + hole, a.get(first + second - 1));
+        hole = second - 1;
+    }
+    int64_t parent = (hole - 1) / 2;
+    while (hole > top && comp(a.get(first + parent), value)) {
+        a.set(first + hole, a.get(first + parent));
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    a.set(first + hole, value);
+}
+
+// std::__make_heap
+__device__ void make_heap(const Arr& a, int64_t first, int64_t last) {
+    const int64_t len = last - first;
+    if (len < 2) return;
+    for (int64_t parent = (len - 2) / 2;; --parent) {
+        adjust_heap(a, first, parent, len, a.get(first + parent));
+        if (parent == 0) return;
+    }
+}
+
+// std::__heap_select: the heap of [first, middle) keeps the best; an element replaces the heap's
+// top (its worst) only if strictly better (std::__pop_heap into the element's slot)
+__device__ void heap_select(const Arr& a, int64_t first, int64_t middle, int64_t last) {
+    make_heap(a, first, middle);
+    for (int64_t i = middle; i < last; ++i) {
+        if (comp(a.get(i), a.get(first))) {
+            const El v = a.get(i);
+            a.set(i, a.get(first));
+            adjust_heap(a, first, 0, middle - first, v);
+        }
+    }
+}
+
+// std::__move_median_to_first
+__device__ void move_median_to_first(const Arr& a, int64_t r, int64_t x, int64_t y, int64_t z) {
+    const El A = a.get(x), B = a.get(y), C = a.get(z);
+    if (comp(A, B)) {
+        if (comp(B, C)) a.swap(r, y);
+        else if (comp(A, C)) a.swap(r, z);
+        else a.swap(r, x);
+    } else if (comp(A, C)) {
+        a.swap(r, x);
+    } else if (comp(B, C)) {
+        a.swap(r, z);
+    } else {
+        a.swap(r, y);
+    }
+}
+
+// std::__unguarded_partition around the pivot at `pivot`
+__device__ int64_t unguarded_partition(const Arr& a, int64_t first, int64_t last, int64_t pivot) {
+    const El pv = a.get(pivot);  // the pivot slot is outside [first, last): never swapped here
+    while (true) {
+        while (comp(a.get(first), pv)) ++first;
+        --last;
+        while (comp(pv, a.get(last))) --last;
+        if (!(first < last)) return first;
+        a.swap(first, last);
+        ++first;
+    }
+}
+
+// std::__insertion_sort (with __unguarded_linear_insert)
+__device__ void insertion_sort(const Arr& a, int64_t first, int64_t last) {
+    if (first == last) return;
+    for (int64_t i = first + 1; i != last; ++i) {
+        const El v = a.get(i);
+        if (comp(v, a.get(first))) {
+            for (int64_t j = i; j > first; --j) a.set(j, a.get(j - 1));  // std::move_backward
+            a.set(first, v);
+        } else {
+            int64_t j = i, nx = i - 1;
+            while (comp(v, a.get(nx))) {
+                a.set(j, a.get(nx));
+                j = nx;
+                --nx;
+            }
+            a.set(j, v);
+        }
+    }
+}
+
+__device__ __forceinline__ int64_t lg(int64_t n) { return 63 - __clzll(static_cast<unsigned long long>(n)); }
+
+// std::nth_element -> std::__introselect(first, nth, last, 2 * __lg(last - first))
+__device__ void nth_element(const Arr& a, int64_t first, int64_t nth, int64_t last) {
+    if (first == last || nth == last) return;
+    int64_t depth = 2 * lg(last - first);
+    while (last - first > 3) {
+        if (depth == 0) {
+            heap_select(a, first, nth + 1, last);
+            a.swap(first, nth);  // the nth element to its final place
+            return;
+        }
+        --depth;
+        const int64_t mid = first + (last - first) / 2;
+        move_median_to_first(a, first, first + 1, mid, last - 1);
+        const int64_t cut = unguarded_partition(a, first + 1, last, first);
+        if (cut <= nth) first = cut;
+        else last = cut;
+    }
+    insertion_sort(a, first, last);
+}
+
+}  // namespace stl
+
+constexpr int kStlHeapMax = 4096;  // k of the partial_sort path (k * 64 <= M): 32 KB of LDS
+
+// partial_sort path: one wave per query streams its dense key row in index order; an element is
+// compared with the heap's top in parallel (64 per step), and the few that beat it are inserted in
+// index order by lane 0 (std::__heap_select's loop, with the heap in LDS).
+__global__ __launch_bounds__(64) void k_select_stl_heap(const uint32_t* __restrict__ list_key, int64_t cap, int64_t M,
+                                                        int32_t k, int64_t P, int64_t Qvalid,
+                                                        int32_t* __restrict__ hits_out) {
+    __shared__ uint32_t hk[kStlHeapMax];
+    __shared__ int32_t hi[kStlHeapMax];
+    const int64_t q = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (q >= Qvalid) {
+        if (lane == 0) hits_out[q] = 0;
+        return;
+    }
+    const uint32_t* row = list_key + q * cap;
+    for (int t = lane; t < k; t += 64) {
+        hk[t] = stl::canon(row[t]);
+        hi[t] = t;
+    }
+    __syncthreads();
+    const stl::Arr heap{hk, hi};
+    if (lane == 0) stl::make_heap(heap, 0, k);
+    __syncthreads();
+    constexpr int U = 8;  // 64-key steps loaded together
+    for (int64_t base = k; base < M; base += 64 * U) {
+        uint32_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = base + u * 64 + lane;
+            v[u] = j < M ? stl::canon(row[j]) : 0u;  // key 0 is below every score's key
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            unsigned long long m = __ballot(v[u] > hk[0]);
+            while (m) {
+                const int l = __ffsll(static_cast<long long>(m)) - 1;
+                m &= m - 1ull;
+                const uint32_t vl = __shfl(v[u], l, 64);
+                if (lane == 0 && vl > hk[0])
+                    stl::adjust_heap(heap, 0, 0, k, stl::El{vl, static_cast<int32_t>(base + u * 64 + l)});
+            }
+            __syncthreads();  // lane 0's heap writes before the next top read
+        }
+    }
+    int32_t h = 0;
+    for (int t = lane; t < k; t += 64) h += hi[t] < P ? 1 : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off, 64);
+    if (lane == 0) hits_out[q] = h;
+}
+
+// nth_element path (k * 64 > M, so M < 64 k): lane 0 runs std::nth_element in place on the
+// query's dense (key, index) row in global memory; the top k are then its first k slots.
+__global__ __launch_bounds__(64) void k_select_stl_nth(uint32_t* __restrict__ list_key, int32_t* __restrict__ list_idx,
+                                                       int64_t cap, int64_t M, int32_t k, int64_t P, int64_t Qvalid,
+                                                       int32_t* __restrict__ hits_out) {
+    const int64_t q = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (q >= Qvalid) {
+        if (lane == 0) hits_out[q] = 0;
+        return;
+    }
+    uint32_t* kr = list_key + q * cap;
+    int32_t* ir = list_idx + q * cap;
+    for (int64_t t = lane; t < M; t += 64) {
+        kr[t] = stl::canon(kr[t]);
+        ir[t] = static_cast<int32_t>(t);
+    }
+    __syncthreads();
+    if (lane == 0) stl::nth_element(stl::Arr{kr, ir}, 0, k - 1, M);
+    __syncthreads();
+    int32_t h = 0;
+    for (int t = lane; t < k; t += 64) h += ir[t] < P ? 1 : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off, 64);
+    if (lane == 0) hits_out[q] = h;
+}
+
 template <int D>
 int launch_filter(const float* Qn, int64_t Qpad, int64_t Qvalid, const float* Cn, int64_t M, int64_t stride,
                   const uint32_t* thr, uint32_t* lk, int32_t* li, int32_t* ln, int32_t cap, hipStream_t s) {
@@ -424,6 +650,24 @@ int lgcn_select_topk(const uint32_t* list_key, const int32_t* list_idx, const in
     k_select_topk<<<dim3(static_cast<unsigned>(Qpad)), kSelBlock, 0, as_stream(stream)>>>(
         list_key, list_idx, list_n, dense_n, cap, k, P, Qvalid, thr_out, hits_out);
     return check_launch("k_select_topk");
+}
+
+int lgcn_select_topk_stl(uint32_t* list_key, int32_t* list_idx, int64_t cap, int64_t M, int32_t k, int64_t P,
+                         int64_t Qpad, int64_t Qvalid, int32_t* hits_out, lgcn_stream_t stream) {
+    if (!list_key || !list_idx || !hits_out || k <= 0 || M < k || cap < M || Qpad <= 0 || Qvalid > Qpad ||
+        Qpad > INT32_MAX || M > INT32_MAX)
+        return fail(LGCN_E_ARG, "lgcn_select_topk_stl: bad args");
+    const bool heap = static_cast<int64_t>(k) * 64 <= M;  // ATen topk_impl_loop's use_partial_sort
+    if (heap) {
+        if (k > kStlHeapMax)
+            return fail(LGCN_E_UNSUPPORTED, "lgcn_select_topk_stl: k=%d > %d on the partial_sort path", k, kStlHeapMax);
+        k_select_stl_heap<<<dim3(static_cast<unsigned>(Qpad)), 64, 0, as_stream(stream)>>>(list_key, cap, M, k, P,
+                                                                                           Qvalid, hits_out);
+        return check_launch("k_select_stl_heap");
+    }
+    k_select_stl_nth<<<dim3(static_cast<unsigned>(Qpad)), 64, 0, as_stream(stream)>>>(list_key, list_idx, cap, M, k, P,
+                                                                                      Qvalid, hits_out);
+    return check_launch("k_select_stl_nth");
 }
 
 }  // extern "C"

@@ -55,11 +55,19 @@ def _normalize_into(lib, x: torch.Tensor, idx, rows: int, out_ptr: int, D: int, 
 
 
 def topk_hits(users: torch.Tensor, picked: torch.Tensor, pos: torch.Tensor, neg: torch.Tensor, k: int,
-              cap: int | None = None, subset: int | None = None) -> torch.Tensor:
+              cap: int | None = None, subset: int | None = None, ties: str | None = None) -> torch.Tensor:
     """hits[q] = number of positives (rows of ``pos``) among the top-k cosine scores of
-    users[picked[q]] against cat(pos, neg); int32 [Q] on the device."""
+    users[picked[q]] against cat(pos, neg); int32 [Q] on the device.
+    ties (default lgcn_amd.tuning's recall_ties): which of several EQUAL scores at the k-th place
+    count — "index": the lowest candidate indices, i.e. the positives (torch.topk on a GPU, the
+    reference's device when it has one); "cpu": the slots CPU torch.topk fills (libstdc++
+    partial_sort / nth_element, lgcn_select_topk_stl). They differ only where a candidate row
+    repeats another (an item that is one edge's positive and another's sampled negative)."""
     from . import tuning
 
+    ties = tuning.get().recall_ties if ties is None else ties
+    if ties not in ("index", "cpu"):
+        raise ValueError(f"recall: ties must be 'index' or 'cpu', got {ties!r}")
     subset = tuning.get().recall_subset if subset is None else int(subset)
     cap = max(subset, CAP_MIN) if cap is None else int(cap)
     lib = _ffi.load()
@@ -86,6 +94,8 @@ def topk_hits(users: torch.Tensor, picked: torch.Tensor, pos: torch.Tensor, neg:
     _normalize_into(lib, users, picked.data_ptr(), Q, ws.Qn.data_ptr(), D, Qpad, s)
     _normalize_into(lib, pos, None, P, ws.Cn.data_ptr(), D, P, s)
     _normalize_into(lib, neg, None, Nn, ws.Cn.data_ptr() + P * D * 4, D, Nn, s)
+    if ties == "cpu":
+        return _hits_cpu_ties(lib, ws, M, D, k, P, Q, Qpad, qmul, s)
     # first thresholds: the k-th best of a strided subset (a lower bound of the true k-th best)
     stride = max(1, -(-M // min(subset, cap)))
     S = -(-M // stride)
@@ -107,6 +117,31 @@ def topk_hits(users: torch.Tensor, picked: torch.Tensor, pos: torch.Tensor, neg:
         _ffi.check(lib.lgcn_select_topk(ws.lkey.data_ptr(), ws.lidx.data_ptr(), ws.lcnt.data_ptr(), 0, cap, k,
                                         P, Qpad, Q, ws.thr.data_ptr(), None, s), "lgcn_select_topk")
     raise RuntimeError("recall: candidate lists kept overflowing (scores too concentrated for the capacity)")
+
+
+# dense score rows of one query block in the "cpu" tie mode (8 bytes per score: key + index)
+STL_BLOCK_BYTES = 1 << 30
+
+
+def _hits_cpu_ties(lib, ws, M: int, D: int, k: int, P: int, Q: int, Qpad: int, qmul: int, s) -> torch.Tensor:
+    """topk_hits with CPU torch.topk's tie rule: each query block's scores are written densely in
+    candidate order (lgcn_score_filter, dense mode — the same f32 MFMA scores as the filtered
+    path), then lgcn_select_topk_stl replays libstdc++'s selection on every row."""
+    blk = max(qmul, (STL_BLOCK_BYTES // (8 * max(M, 1))) // qmul * qmul)
+    blk = min(blk, Qpad)
+    dev = ws.Qn.device
+    keys = torch.empty((blk, M), dtype=torch.int32, device=dev)
+    idx = torch.empty((blk, M), dtype=torch.int32, device=dev)
+    hits = torch.empty(Qpad, dtype=torch.int32, device=dev)
+    for q0 in range(0, Qpad, blk):
+        nb = min(blk, Qpad - q0)
+        qv = max(0, min(nb, Q - q0))
+        qptr = ws.Qn.data_ptr() + q0 * D * 4
+        _ffi.check(lib.lgcn_score_filter(qptr, nb, qv, ws.Cn.data_ptr(), M, 1, D, None, keys.data_ptr(),
+                                         idx.data_ptr(), None, M, s), "lgcn_score_filter(dense)")
+        _ffi.check(lib.lgcn_select_topk_stl(keys.data_ptr(), idx.data_ptr(), M, M, k, P, nb, qv,
+                                            hits.data_ptr() + q0 * 4, s), "lgcn_select_topk_stl")
+    return hits[:Q].clone()
 
 
 def legacy_choice(n: int, size: int, draws: int) -> np.ndarray:
@@ -169,11 +204,13 @@ def compute_recall_at_k(embs, k: int = 20, num_samples: int = 10, sample_size: i
     else:
         picked = legacy_choice(user_embs.size(0), sample_size, num_samples).reshape(-1)
     hits = topk_hits(user_embs, torch.from_numpy(picked), pos_item_embs, neg_item_embs, k)
-    if int(hits.min().item()) < 0:
+    hits = hits.cpu()  # the one host read of the call
+    if int(hits.min()) < 0:
         raise RuntimeError("recall: a query ranked fewer than k candidates")
+    # the reference's float32 arithmetic on the host, per sample as it runs it (hits / P, then a
+    # 1-D CPU mean): equal hit counts give the CPU reference's value to the bit
     per_user = hits.to(torch.float32) / num_pos
-    means = [m for m in per_user.view(num_samples, sample_size).mean(dim=1).double().cpu().tolist()]
     total = 0.0
-    for m in means:
-        total += m
+    for row in per_user.view(num_samples, sample_size):
+        total += row.contiguous().mean().item()
     return total / num_samples

@@ -44,6 +44,11 @@ class Tuning:
     batch_chunk: int | None = None
     # Recall@k: candidates in the strided subset that sets the first thresholds
     recall_subset: int = 16384
+    # Recall@k: which of several equal scores make a query's top k (lgcn_amd.recall.topk_hits):
+    # "index" — the lowest candidate indices (the positives) first, as torch.topk on a GPU (its
+    # gather pass fills the k-th value's ties in index order); "cpu" — exactly what CPU torch.topk
+    # keeps (libstdc++ partial_sort / nth_element, lgcn_select_topk_stl)
+    recall_ties: str = "index"
     # utils.train_test.train routes eligible calls to the fused batch step (False: reference loop)
     harness_fused: bool = True
     # run the exchanges' RCCL branches even on a gloo group (tests: gloo carries the bytes)
@@ -63,6 +68,8 @@ class Tuning:
             raise ValueError(f"neg_grouping must be 'count' or 'radix', got {self.neg_grouping!r}")
         if self.sorted_scatter_min_b < 1 or self.recall_subset < 1:
             raise ValueError("sorted_scatter_min_b and recall_subset must be >= 1")
+        if self.recall_ties not in ("index", "cpu"):
+            raise ValueError(f"recall_ties must be 'index' or 'cpu', got {self.recall_ties!r}")
         if self.batch_chunk is not None and self.batch_chunk < 1:
             raise ValueError(f"batch_chunk must be None or >= 1, got {self.batch_chunk}")
 
@@ -99,7 +106,7 @@ def set_tuning(**changes) -> Tuning:
         raise TypeError(f"unknown tuning field(s): {sorted(unknown)}")
     new = dataclasses.replace(_current, **changes)
     new.validate()
-    if any(k in NATIVE for k in changes) or any(getattr(new, f) != getattr(_current, f) for f in NATIVE):
+    if any(getattr(new, f) != getattr(_current, f) for f in NATIVE):  # only a real change loads the library
         _apply_native(new)
     prev, _current = _current, new
     return prev

@@ -281,3 +281,100 @@ def test_harness_one_shot_loader_falls_back_mid_epoch(gpu, tune):
     assert TT.LAST_TRAIN_PATH == "fused"
     for p in (model.user_embedding.weight, model.item_embedding.weight):
         assert int(float(opt.state[p]["step"])) == 7
+
+
+def test_harness_epoch_and_evaluate_match_reference_golden(gpu, tune, monkeypatch):
+    """the reference's own train() epoch and evaluate() outputs
+    (tests/golden/harness.npz, recorded by running reference utils/train_test.py on the CPU oracle
+    model: torch.manual_seed(41) -> train over the three golden batches, then torch.manual_seed(42),
+    np.random.seed(43) -> evaluate on the validation edges) reproduced by this package's fused GPU
+    train() and GPU evaluate(). The negatives are the reference's draws: the CPU global generator,
+    moved to the device. Bars: the epoch loss and the validation loss within 1e-5 relative; the
+    tables under the trajectory bar (settled elements — every step's gradient clear of the row bar
+    in the reference run, no near-cancelling first moment — within 1e-5 of their row's scale);
+    Recall@100's hit counts exact with recall_ties="cpu" (CPU torch.topk's choice among equal scores: the
+    golden ran on a CPU), and with the default "index" rule equal to the oracle tables scored through
+    that same rule."""
+    from models.light_gcn import LightGCN
+    from oracle.lgconv_torch import OracleLightGCN
+    from parity import record_stats, trajectory_bar
+    from utils import helpers
+    from utils import train_test as TT
+
+    monkeypatch.setattr(helpers, "sample_negative",
+                        lambda pos_idx, num_items, device: torch.randint(0, num_items, (pos_idx.shape[0],)).to(device))
+    G = np.load(GOLDEN / "harness.npz")
+    U, I = int(G["train_U"]), int(G["train_I"])
+    w0 = [G["train_init_user_w"], G["train_init_item_w"]]
+    loader = [_Batch(torch.from_numpy(G[f"train_batch{p}"])) for p in range(3)]
+    val = _Batch(torch.from_numpy(G["val_edge_index"]))
+
+    def make(cls, dev):
+        m = cls(U, I, num_layers=3, dim_h=64).to(dev)
+        with torch.no_grad():
+            m.user_embedding.weight.copy_(torch.from_numpy(w0[0]))
+            m.item_embedding.weight.copy_(torch.from_numpy(w0[1]))
+        return m
+
+    # the reference run's per-step gradients (CPU oracle) for the settled-element mask. Its tables
+    # equal the golden's bitwise on the host that recorded it (tests/test_harness.py); on another
+    # host CPU torch's vectorised reductions may round differently, so they are not asserted here
+    ref = make(OracleLightGCN, torch.device("cpu"))
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    grads, inner = [], ropt.step
+
+    def step(*a, **k):
+        grads.append([p.grad.detach().clone() for p in (ref.user_embedding.weight, ref.item_embedding.weight)])
+        return inner(*a, **k)
+
+    ropt.step = step
+    torch.manual_seed(41)
+    TT.train(ref, ropt, loader, torch.device("cpu"))
+
+    tune(harness_fused=True)
+    hip = make(LightGCN, gpu)
+    opt = torch.optim.Adam(hip.parameters(), lr=1e-3)
+    torch.manual_seed(41)
+    loss = TT.train(hip, opt, loader, gpu)
+    assert TT.LAST_TRAIN_PATH == "fused", TT.LAST_TRAIN_PATH
+    gl = float(G["train_epoch_loss"])
+    assert abs(loss - gl) <= 1e-5 * abs(gl), (loss, gl)
+    masks = _settled(grads)
+    stats = {"epoch_loss": loss, "epoch_loss_golden": gl}
+    for t, (name, key) in enumerate((("user", "train_user_w"), ("item", "train_item_w"))):
+        got = getattr(hip, f"{name}_embedding").weight.detach().cpu().numpy()
+        stats[f"{name}.w"] = trajectory_bar(got, G[key], w0[t], masks[t], 1e-3, len(grads), f"golden epoch {name}")
+    out = {}
+    for ties in ("cpu", "index"):
+        tune(recall_ties=ties)
+        torch.manual_seed(42)
+        np.random.seed(43)
+        out[ties] = TT.evaluate(hip, val, gpu)
+    # the oracle tables through the "index" rule on the GPU (the same negatives and picks)
+    golden_model = _loaded(LightGCN, U, I, G, gpu)  # built before seeding: its init draws from the generator
+    torch.manual_seed(42)
+    np.random.seed(43)
+    oracle_index = TT.evaluate(golden_model, val, gpu)
+    vl, vr = float(G["val_loss"]), float(G["val_recall100"])
+    stats.update(val_loss=out["cpu"][0], val_loss_golden=vl, recall100_cpu_ties=out["cpu"][1],
+                 recall100_golden=vr, recall100_index=out["index"][1], recall100_index_oracle_tables=oracle_index[1])
+    record_stats("harness_golden_epoch_evaluate", stats)
+    print(f"golden epoch: loss {loss:.9f} vs {gl:.9f}; val loss {out['cpu'][0]:.9f} vs {vl:.9f}; Recall@100 "
+          f"cpu ties {out['cpu'][1]:.9f} vs golden {vr:.9f}; index ties {out['index'][1]:.9f} "
+          f"(oracle tables {oracle_index[1]:.9f}); {stats}")
+    for ties in ("cpu", "index"):
+        assert abs(out[ties][0] - vl) <= 1e-5 * abs(vl), (ties, out[ties][0], vl)
+    # hit counts exact: one hit moves Recall@100 by 1 / (P * 100 * 10) — 1e-5 relative here — and
+    # the 1e-9 left is the host CPU's float32 mean of 100 per-user values (another host, another
+    # vector width)
+    assert out["cpu"][1] == pytest.approx(vr, rel=1e-7, abs=0), (out["cpu"][1], vr)
+    assert out["index"][1] == oracle_index[1], (out["index"][1], oracle_index[1])
+
+
+def _loaded(cls, U, I, G, dev):
+    """A model holding the golden post-epoch tables (the reference's own)."""
+    m = cls(U, I, num_layers=3, dim_h=64).to(dev)
+    with torch.no_grad():
+        m.user_embedding.weight.copy_(torch.from_numpy(G["train_user_w"]))
+        m.item_embedding.weight.copy_(torch.from_numpy(G["train_item_w"]))
+    return m

@@ -119,9 +119,11 @@ def test_compute_recall_at_k_matches_oracle_at_scale(gpu):
         assert np.abs(hits[~sep] - hits_ref[~sep]).max(initial=0) <= 1
         unseparated += int((~sep).sum())
         rows.append(hits_d)
-    # the reference's per-sample float32 means, formed on the device as lgcn_amd.recall forms them
-    means = (torch.stack(rows).to(torch.float32) / pos.shape[0]).mean(dim=1).double().cpu().tolist()
-    assert got == sum(means) / len(detail)
+    # the reference's per-sample float32 means (hits / P, a 1-D CPU mean per sample), summed in order
+    total = 0.0
+    for r in rows:
+        total += (r.cpu().to(torch.float32) / pos.shape[0]).mean().item()
+    assert got == total / len(detail)
     # each unseparated query moves its user's recall by at most 1/P, the result by that / (100 * samples)
     bound = unseparated / (pos.shape[0] * 100 * len(detail))
     assert abs(got - ref) <= bound + 1e-6 * abs(ref)
@@ -159,3 +161,94 @@ def test_evaluate_overlapped_draws_equal_sequential(gpu):
     state_b = np.random.get_state()
     assert loss_a == loss_b and rec_a == rec_b
     assert state_a[2] == state_b[2] and np.array_equal(state_a[1], state_b[1])
+
+
+def _key_scores(keys: np.ndarray) -> np.ndarray:
+    """float32 scores from lgcn_score_filter's order-preserving keys (csrc/lgcn_recall.hip key_score)."""
+    k = keys.view(np.uint32)
+    bits = np.where(k & np.uint32(0x80000000), k ^ np.uint32(0x80000000), ~k).astype(np.uint32)
+    return bits.view(np.float32)
+
+
+def _dup_rows(rng, n_items, d, P, Nn, Q):
+    items = _emb(rng, n_items, d)
+    return _emb(rng, Q, d), items[rng.integers(0, n_items, P)], items[rng.integers(0, n_items, Nn)]
+
+
+@pytest.mark.parametrize("P,Nn,k,Q", [(1250, 1250, 20, 200), (1250, 1250, 100, 200), (4500, 4500, 100, 130),
+                                      (150, 150, 5, 64), (40000, 40000, 20, 128)])
+def test_select_topk_stl_matches_cpu_topk_model(gpu, P, Nn, k, Q):
+    """lgcn_select_topk_stl on the GPU's own dense scores == oracle/topk_cpu.py (the libstdc++
+    selection CPU torch.topk runs, pinned to torch.topk in tests/test_recall_stl.py) on the same
+    scores, query by query: candidate rows repeat (every repeated row's scores tie exactly), and the
+    cases cover the partial_sort path (k * 64 <= M: M = 2,500 / k = 20, M = 80,000), the
+    nth_element path (M = 2,500 / k = 100, M = 9,000, M = 300) and padded query blocks."""
+    from lgcn_amd import _ffi
+    from oracle import topk_cpu
+
+    rng = np.random.default_rng(P + k + Q)
+    d = 32
+    users, pos, neg = _dup_rows(rng, max(8, (P + Nn) // 8), d, P, Nn, Q)
+    lib = _ffi.load()
+    s = _ffi.stream_of(gpu)
+    t = lambda a: torch.from_numpy(a).to(gpu)
+    M = P + Nn
+    D, Qpad = 32, -(-Q // 128) * 128
+    Qn = torch.empty((Qpad, D), dtype=torch.float32, device=gpu)
+    Cn = torch.empty((M, D), dtype=torch.float32, device=gpu)
+    u, pp, nn_ = t(users), t(pos), t(neg)
+    _ffi.check(lib.lgcn_normalize_rows(u.data_ptr(), None, Q, d, d, Qn.data_ptr(), D, Qpad, s), "normalize")
+    _ffi.check(lib.lgcn_normalize_rows(pp.data_ptr(), None, P, d, d, Cn.data_ptr(), D, P, s), "normalize")
+    _ffi.check(lib.lgcn_normalize_rows(nn_.data_ptr(), None, Nn, d, d, Cn.data_ptr() + P * D * 4, D, Nn, s), "normalize")
+    keys = torch.empty((Qpad, M), dtype=torch.int32, device=gpu)
+    idx = torch.empty((Qpad, M), dtype=torch.int32, device=gpu)
+    _ffi.check(lib.lgcn_score_filter(Qn.data_ptr(), Qpad, Q, Cn.data_ptr(), M, 1, D, None, keys.data_ptr(),
+                                     idx.data_ptr(), None, M, s), "lgcn_score_filter")
+    scores = _key_scores(keys[:Q].cpu().numpy())
+    hits = torch.full((Qpad,), -7, dtype=torch.int32, device=gpu)
+    _ffi.check(lib.lgcn_select_topk_stl(keys.data_ptr(), idx.data_ptr(), M, M, k, P, Qpad, Q, hits.data_ptr(), s),
+               "lgcn_select_topk_stl")
+    got = hits.cpu().numpy()
+    assert (got[Q:] == 0).all()
+    want = topk_cpu.topk_hits(scores, k, P)
+    np.testing.assert_array_equal(got[:Q], want)
+    # and the lowest-index rule (lgcn_select_topk) counts differently on these rows
+    low = topk_hits_index(gpu, users, pos, neg, k)
+    assert (low >= got[:Q]).all() and (low != got[:Q]).any()
+
+
+def topk_hits_index(gpu, users, pos, neg, k):
+    from lgcn_amd.recall import topk_hits
+
+    t = lambda a: torch.from_numpy(a).to(gpu)
+    return topk_hits(t(users), torch.arange(users.shape[0]), t(pos), t(neg), k, ties="index").cpu().numpy()
+
+
+def test_compute_recall_at_k_cpu_ties_equals_reference_on_cpu(gpu, tune):
+    """Recall@20 / @100 of duplicate-heavy validation rows (600 items behind 2 x 1,250 candidate
+    rows, as a C1 validation batch has them): compute_recall_at_k on device tensors with
+    recall_ties="cpu" equals the reference's formula run on the CPU (utils/train_test.py's CPU
+    branch: torch.mm + torch.topk), to the bit; the default "index" rule equals the lowest-index
+    restatement oracle/recall_ref.py, and the two differ on these rows."""
+    from utils import train_test as TT
+
+    rng = np.random.default_rng(21)
+    users, pos, neg = _dup_rows(rng, 600, 64, 1250, 1250, 1250)
+    host = tuple(torch.from_numpy(a) for a in (users, pos, neg))
+    dev = tuple(a.to(gpu) for a in host)
+    for k in (20, 100):
+        np.random.seed(9)
+        ref_cpu = TT.compute_recall_at_k(host, k=k)
+        np.random.seed(9)
+        tune(recall_ties="cpu")
+        got_cpu = TT.compute_recall_at_k(dev, k=k)
+        np.random.seed(9)
+        tune(recall_ties="index")
+        got_index = TT.compute_recall_at_k(dev, k=k)
+        np.random.seed(9)
+        ref_index = R.recall_at_k((users, pos, neg), k=k)
+        print(f"Recall@{k}: cpu ties {got_cpu:.8f} (reference on CPU {ref_cpu:.8f}); "
+              f"index ties {got_index:.8f} (oracle {ref_index:.8f})")
+        assert got_cpu == ref_cpu, (k, got_cpu, ref_cpu)
+        assert got_index == pytest.approx(ref_index, rel=1e-6, abs=0), (k, got_index, ref_index)
+        assert got_index != got_cpu
