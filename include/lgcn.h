@@ -90,6 +90,17 @@ int lgcn_abi_version(void);
  * lgcn_common.h and this header (build provenance; lgcn_amd._ffi refuses a mismatch). */
 const char* lgcn_source_sha256(void);
 
+/* 128-bit content digest of nbytes at data (ABI 9), on the device: out[0..1] (device uint64[2])
+ * from two independent sums mod 2^64 of keyed murmur3-fmix64 mixes of the 8-byte words and their
+ * positions (the < 8 trailing bytes as one more word), the length folded in — deterministic, order
+ * sensitive. ws: device uint64[>= 2 * LGCN_DIGEST_BLOCKS]; data 8-byte aligned. Stream-ordered, no
+ * sync. Replaces the host copy + XXH3 with which lgcn_amd._cache keyed a device edge_index by
+ * content (the per-batch caches behind reference data/dataset_handler.py:285's loader, which
+ * collates new tensors every epoch). */
+#define LGCN_DIGEST_BLOCKS 1024
+int lgcn_digest128(const void* data, int64_t nbytes, uint64_t* ws, int64_t ws_words, uint64_t* out,
+                   lgcn_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * Tuning (ABI 7). The schedule choices earlier builds read from environment variables at every
  * dispatch (A/B knobs) are one process-wide struct now; the library reads no environment.

@@ -514,11 +514,105 @@ __global__ void k_group_order(const int64_t* __restrict__ rowptr, int64_t R, int
     }
 }
 
+// ---- content digest of a device buffer (lgcn_digest128) ---------------------------------------
+// The per-batch caches find a batch's plans / captured graph by the CONTENT of its edge_index
+// (lgcn_amd._cache). For a device tensor that was a copy to the host and XXH3 there, one sync per
+// new tensor object; this is the on-device digest: two independent 64-bit lanes, each the sum
+// mod 2^64 over the 8-byte words w_i of a keyed mix f(w_i, i) (murmur3's fmix64 finaliser), then
+// the length folded in. Sums mod 2^64 associate exactly, so the digest is deterministic for any
+// grid; the word index inside the mix makes it order-sensitive. Not cryptographic (nor is XXH3):
+// an accidental collision needs two equal-shaped batches with equal 128-bit sums.
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+__device__ __forceinline__ void digest_word(uint64_t w, uint64_t i, uint64_t& a, uint64_t& b) {
+    a += fmix64(w ^ fmix64(i * 0x9e3779b97f4a7c15ull + 0x243f6a8885a308d3ull));
+    b += fmix64((w + 0x632be59bd9b4e019ull) * 0xd6e8feb86659fd93ull ^ fmix64(i + 0x8cb92ba72f3d8dd7ull));
+}
+
+__device__ __forceinline__ void block_sum2(uint64_t& a, uint64_t& b) {
+    __shared__ uint64_t red[kBlock / 64][2];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off, 64);
+        b += __shfl_xor(b, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6][0] = a;
+        red[threadIdx.x >> 6][1] = b;
+    }
+    __syncthreads();
+    a = b = 0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < kBlock / 64; ++w) {
+            a += red[w][0];
+            b += red[w][1];
+        }
+}
+
+__global__ __launch_bounds__(kBlock) void k_digest_partial(const uint64_t* __restrict__ words, int64_t nwords,
+                                                           const uint8_t* __restrict__ tail, int32_t ntail,
+                                                           uint64_t* __restrict__ ws) {
+    uint64_t a = 0, b = 0;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nwords; i += int64_t(gridDim.x) * kBlock)
+        digest_word(words[i], static_cast<uint64_t>(i), a, b);
+    if (ntail > 0 && blockIdx.x == 0 && threadIdx.x == 0) {  // the last < 8 bytes as one word
+        uint64_t w = 0;
+        for (int j = 0; j < ntail; ++j) w |= static_cast<uint64_t>(tail[j]) << (8 * j);
+        digest_word(w, static_cast<uint64_t>(nwords), a, b);
+    }
+    block_sum2(a, b);
+    if (threadIdx.x == 0) {
+        ws[2 * blockIdx.x] = a;
+        ws[2 * blockIdx.x + 1] = b;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_digest_final(const uint64_t* __restrict__ ws, int32_t nblocks,
+                                                         int64_t nbytes, uint64_t* __restrict__ out) {
+    uint64_t a = 0, b = 0;
+    for (int i = threadIdx.x; i < nblocks; i += kBlock) {
+        a += ws[2 * i];
+        b += ws[2 * i + 1];
+    }
+    block_sum2(a, b);
+    if (threadIdx.x == 0) {
+        out[0] = fmix64(a ^ static_cast<uint64_t>(nbytes));
+        out[1] = fmix64(b + static_cast<uint64_t>(nbytes) * 0x9e3779b97f4a7c15ull);
+    }
+}
+
 }  // namespace
 
 extern "C" {
 
 const char* lgcn_last_error(void) { return err_buf(); }
+
+int lgcn_digest128(const void* data, int64_t nbytes, uint64_t* ws, int64_t ws_words, uint64_t* out,
+                   lgcn_stream_t stream) {
+    if (nbytes < 0 || (nbytes > 0 && !data) || !ws || !out || (reinterpret_cast<uintptr_t>(data) & 7) ||
+        ws_words < 2 * LGCN_DIGEST_BLOCKS)
+        return fail(LGCN_E_ARG, "lgcn_digest128: bad args (nbytes=%lld ws_words=%lld, data 8-byte aligned)",
+                    (long long)nbytes, (long long)ws_words);
+    const int64_t nwords = nbytes / 8;
+    int64_t blocks = (nwords + kBlock * 8 - 1) / (kBlock * 8);  // >= 8 words per thread
+    if (blocks < 1) blocks = 1;
+    if (blocks > LGCN_DIGEST_BLOCKS) blocks = LGCN_DIGEST_BLOCKS;
+    hipStream_t s = as_stream(stream);
+    const uint8_t* bytes = static_cast<const uint8_t*>(data);
+    k_digest_partial<<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(
+        static_cast<const uint64_t*>(data), nwords, bytes + nwords * 8, static_cast<int32_t>(nbytes & 7), ws);
+    int rc = check_launch("k_digest_partial");
+    if (rc != LGCN_OK) return rc;
+    k_digest_final<<<1, kBlock, 0, s>>>(ws, static_cast<int32_t>(blocks), nbytes, out);
+    return check_launch("k_digest_final");
+}
 int lgcn_abi_version(void) { return LGCN_ABI_VERSION; }
 
 int lgcn_csr_workspace_size(int64_t E, int64_t N, size_t* bytes) {

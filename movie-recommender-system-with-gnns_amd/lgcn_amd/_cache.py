@@ -6,14 +6,22 @@ iteration; keyed by id() every epoch would miss and rebuild what a batch needs (
 copies, captured hipGraphs) while the dead entries piled up. Here an entry is found by:
 
   1. the tensor object itself (id + weakref + in-place version counter): no hashing, no sync;
-  2. else its content key: (device, dtype, shape, 128-bit XXH3 digest of its bytes; BLAKE2b
-     where the xxhash module is absent) — a CPU tensor is hashed in place (a C3 batch's 320 KB
-     in ~25 us); a device tensor is copied to the host once (one sync, paid only on an object
-     miss, which otherwise costs a whole plan build).
+  2. else its content key: (device, dtype, shape, 128-bit digest of its bytes) — a CPU tensor is
+     hashed in place with XXH3 (BLAKE2b where the xxhash module is absent; a C3 batch's 320 KB in
+     ~25 us); a device tensor is digested ON the device (lgcn_digest128: two kernels, then 16 bytes
+     to pinned host memory), no copy of the batch. prefetch(t) starts that digest without
+     waiting, so a harness that reads its loader one batch ahead (lgcn_amd.harness) finds the
+     digest finished when it needs it: no host sync per batch.
 
 Entries live in an LRU of bounded size (least recently used evicted first). The id -> key memo
 is shared by every cache (a tensor is hashed at most once while it lives unmodified) and drops the
 entries of freed tensors as it grows.
+
+What the memo cannot see: it trusts torch's in-place version counter, and some writes do not bump
+it — a write into a torch.from_numpy buffer through numpy, through .data, through DLPack or a raw
+data_ptr. A tensor object reused after such a write keeps its old content key (and so the previous
+batch's plans and captured graph). A loader that refills one buffer that way must hand over a new
+tensor object per batch (a view or a clone), or call forget(t) after each refill.
 """
 from __future__ import annotations
 
@@ -33,14 +41,56 @@ except ImportError:  # pragma: no cover - xxhash ships with the image
         return hashlib.blake2b(buf, digest_size=16).digest()
 
 
+class _PendingDigest:
+    """A device digest in flight: 16 bytes landing in pinned host memory behind an event."""
+
+    __slots__ = ("host", "event", "keep")
+
+    def __init__(self, host, event, keep):
+        self.host, self.event, self.keep = host, event, keep
+
+    def result(self) -> bytes:
+        self.event.synchronize()
+        self.keep = None
+        return self.host.numpy().tobytes()
+
+
+# per device: the digest's workspace (uint64[2 * LGCN_DIGEST_BLOCKS])
+_DIGEST_WS: dict = {}
+
+
+def _device_digest_start(t: torch.Tensor) -> _PendingDigest:
+    """lgcn_digest128 of a device tensor's bytes on its device's current stream; no wait."""
+    from . import _ffi
+
+    lib = _ffi.load()
+    c = t.detach().contiguous()
+    dev = c.device
+    ws = _DIGEST_WS.get(dev)
+    if ws is None:
+        ws = _DIGEST_WS[dev] = torch.empty(2 * _ffi.DIGEST_BLOCKS, dtype=torch.int64, device=dev)
+    out = torch.empty(2, dtype=torch.int64, device=dev)
+    nbytes = c.numel() * c.element_size()
+    _ffi.check(lib.lgcn_digest128(c.data_ptr() if nbytes else None, nbytes, ws.data_ptr(), ws.numel(),
+                                  out.data_ptr(), _ffi.stream_of(dev)), "lgcn_digest128")
+    host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+    host.copy_(out, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    return _PendingDigest(host, ev, (c, out))
+
+
+def _key_parts(t: torch.Tensor) -> tuple:
+    return (str(t.device), str(t.dtype), tuple(t.shape))
+
+
 def content_key(t: torch.Tensor, extra: tuple = ()) -> tuple:
     """(device, dtype, shape, digest of the bytes, *extra): equal for tensors of equal content."""
-    host = t.detach()
-    if host.device.type != "cpu":
-        host = host.cpu()
-    host = host.contiguous()
+    if t.device.type != "cpu":
+        return (*_key_parts(t), _device_digest_start(t).result(), *extra)
+    host = t.detach().contiguous()
     digest = _digest(host.numpy().view("uint8").data if host.numel() else b"")
-    return (str(t.device), str(t.dtype), tuple(t.shape), digest, *extra)
+    return (*_key_parts(t), digest, *extra)
 
 
 # id(tensor) -> (weakref, version, content key): shared by every cache, so a tensor is hashed once
@@ -55,6 +105,26 @@ def _version(t: torch.Tensor):
         return None
 
 
+def _remember(t: torch.Tensor, ver, key) -> None:
+    _KEYS[id(t)] = (weakref.ref(t), ver, key)
+    if len(_KEYS) > 64 and len(_KEYS) % 64 == 0:  # amortised: drop the entries of freed tensors
+        for k in [k for k, (r, _, _) in _KEYS.items() if r() is None]:
+            del _KEYS[k]
+
+
+def prefetch(t: torch.Tensor) -> None:
+    """Start t's content key without waiting (a device tensor's digest is enqueued on the current
+    stream); tensor_key(t) later collects it. A no-op for CPU tensors, inference tensors and
+    tensors whose key is memoised already."""
+    ver = _version(t)
+    if t.device.type == "cpu" or ver is None:
+        return
+    hit = _KEYS.get(id(t))
+    if hit is not None and hit[0]() is t and hit[1] == ver:
+        return
+    _remember(t, ver, (_key_parts(t), _device_digest_start(t)))
+
+
 def tensor_key(t: torch.Tensor) -> tuple:
     """content_key(t), memoised on the tensor object while it lives and is not modified in place."""
     ver = _version(t)
@@ -62,19 +132,29 @@ def tensor_key(t: torch.Tensor) -> tuple:
     if hit is not None and ver is not None:
         ref, v, key = hit
         if ref() is t and v == ver:
+            if isinstance(key, tuple) and len(key) == 2 and isinstance(key[1], _PendingDigest):
+                key = (*key[0], key[1].result())  # a prefetched digest: collect it
+                _KEYS[id(t)] = (ref, v, key)
             return key
     key = content_key(t)
     if ver is not None:
-        _KEYS[id(t)] = (weakref.ref(t), ver, key)
-    if len(_KEYS) > 64 and len(_KEYS) % 64 == 0:  # amortised: drop the entries of freed tensors
-        for k in [k for k, (r, _, _) in _KEYS.items() if r() is None]:
-            del _KEYS[k]
+        _remember(t, ver, key)
     return key
 
 
-def _memo_hit(t: torch.Tensor) -> bool:
+def forget(t: torch.Tensor) -> None:
+    """Drop t's memoised key (after a write the version counter does not see)."""
     hit = _KEYS.get(id(t))
-    return hit is not None and hit[0]() is t and hit[1] == _version(t)
+    if hit is not None and hit[0]() is t:
+        del _KEYS[id(t)]
+
+
+def _memo_hit(t: torch.Tensor) -> bool:
+    """t's key is memoised from an earlier lookup of this object (a prefetched, not yet collected
+    digest is a content lookup, not an object hit)."""
+    hit = _KEYS.get(id(t))
+    return (hit is not None and hit[0]() is t and hit[1] == _version(t)
+            and not (len(hit[2]) == 2 and isinstance(hit[2][1], _PendingDigest)))
 
 
 class ContentLRU:

@@ -26,6 +26,7 @@ E_ARG, E_WORKSPACE, E_UNSUPPORTED = -1, -2, -3  # include/lgcn.h LGCN_E_*
 ITEM_BYTES = 16   # lgcn_item_t {int64 beg; int32 len; int32 dst}
 SPLIT_BYTES = 16  # lgcn_split_t {int32 row, pbeg, pcnt, pad}
 ABI_VERSION = 9  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
+DIGEST_BLOCKS = 1024  # LGCN_DIGEST_BLOCKS
 
 _lib = None
 
@@ -119,6 +120,7 @@ _SIGS = {
     "lgcn_normalize_rows": ([_vp, _vp, _i64, _i64, _i32, _vp, _i32, _i64, _vp], ctypes.c_int),
     "lgcn_score_filter": ([_vp, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp], ctypes.c_int),
     "lgcn_select_topk": ([_vp, _vp, _vp, _i32, _i32, _i32, _i64, _i64, _i64, _vp, _vp, _vp], ctypes.c_int),
+    "lgcn_digest128": ([_vp, _i64, _vp, _i64, _vp, _vp], ctypes.c_int),
     "lgcn_select_topk_stl": ([_vp, _vp, _i64, _i64, _i32, _i64, _i64, _i64, _vp, _vp], ctypes.c_int),
     "lgcn_legacy_choice": ([_vp, _vp, _i64, _i64, _i64, _vp], ctypes.c_int),
     "lgcn_slice_schedule_workspace_size": ([_i64, _i64, _i32, _i32, _vp, _vp], ctypes.c_int),

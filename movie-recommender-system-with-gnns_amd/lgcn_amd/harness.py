@@ -111,8 +111,13 @@ class _Fast:
         if n_batches:
             cap = max(_MIN_STATES, 2 * n_batches)
             for c in (self.step._states, self.dev_batches, self.checked):
-                c.resize(cap)
+                c.resize(max(cap, c.capacity))
             self.reserve(self.opt.steps + n_batches)
+
+    def grow_caches(self, cap: int) -> None:
+        for c in (self.step._states, self.dev_batches, self.checked):
+            if c.capacity < cap:
+                c.resize(cap)
 
     def reserve(self, steps: int) -> None:
         if self.opt.reserve(steps):
@@ -179,13 +184,20 @@ def bipartite(ei: torch.Tensor, U: int) -> bool:
     return bool(((ei[0] < U) == (ei[1] >= U)).all().item())
 
 
+_END = object()
+
+
 def train_epoch(model, optimizer, batches, device):
     """Run the fused step over the batches iterator until it ends or yields a batch the fused step
     cannot take (not a bipartite user-item edge list). Returns (sum over the fused batches of
-    loss * edges as a device tensor or None, their total edges, the first batch not taken or None,
-    fused steps run). The torch optimizer holds the row-lazy Adam's state whenever this returns,
-    so the caller runs the reference loop from the returned batch on (the iterator is read once:
-    one-shot loaders lose no batch)."""
+    loss * edges as a device tensor or None, their total edges, the batches read but not taken —
+    a list, or None —, fused steps run). The torch optimizer holds the row-lazy Adam's state
+    whenever this returns, so the caller runs the reference loop over the returned batches and
+    then the rest of the iterator (it is read once: one-shot loaders lose no batch).
+    The loader is read one batch ahead: a device edge_index of the next batch has its content
+    digest enqueued (lgcn_amd._cache.prefetch) before this step's work, so it is ready when that
+    batch's state is looked up — a loader that collates new device tensors every epoch costs no
+    host sync per step."""
     fast = _FAST.get(optimizer)
     if fast is None or fast.model is not model:
         fast = _Fast(model, optimizer)
@@ -198,12 +210,24 @@ def train_epoch(model, optimizer, batches, device):
     fast.size_for(n)
     total, total_w, steps, leftover = None, 0, 0, None
     U = model.num_users
+    from ._cache import prefetch
+
+    it = iter(batches)
+    nxt = next(it, _END)
     try:
-        for batch in batches:
+        while nxt is not _END:
+            batch = nxt
+            nxt = next(it, _END)
+            if nxt is not _END and getattr(nxt.edge_index, "is_cuda", False):
+                prefetch(nxt.edge_index)
             ei = fast.device_edge_index(batch.edge_index, device)
             if not fast.eligible(ei, U):
-                leftover = batch
+                leftover = [batch] + ([nxt] if nxt is not _END else [])
                 break
+            if n is None and 2 * (steps + 1) > fast.step._states.capacity:
+                # a loader without len(): the batch caches grow with the batches seen (an epoch of
+                # more distinct batches than they hold would miss on every step)
+                fast.grow_caches(2 * fast.step._states.capacity)
             if fast.opt.steps + 1 > fast.opt.max_steps:  # a loader without len(): grow mid-epoch
                 fast.step.sync()  # every row current before the constants are regenerated
                 fast.reserve(fast.opt.steps + 1)

@@ -408,6 +408,7 @@ class FusedTrainStep:
             for a in ("graph", "graph_post", "graph_loss", "graph_grads"):
                 if hasattr(st, a):
                     setattr(st, a, None)
+        self._owner_graphs = None  # the owner update's graph reads the optimizer's constants too
 
     def has_state(self, edge_index: torch.Tensor) -> bool:
         """A state for a batch of this content exists (its checks already passed)."""
@@ -713,11 +714,17 @@ class FusedTrainStep:
             torch.cuda.synchronize()
             steps = opt.steps
             g0, g1 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g0):
-                self._owner_reduce()
-            with torch.cuda.graph(g1):  # records the launches only: no step runs (steps restored)
-                self._owner_update()
-            opt.steps = steps
+            # the capture records the launches of the step just run and runs none: its max_steps
+            # check is taken at that step's index (not one past it, which fails when the table is
+            # exactly full), and the count is restored after
+            opt.steps = steps - 1
+            try:
+                with torch.cuda.graph(g0):
+                    self._owner_reduce()
+                with torch.cuda.graph(g1):
+                    self._owner_update()
+            finally:
+                opt.steps = steps
             self._owner_graphs = (g0, g1)
         ex.pending = nxt
         self._synced = False
@@ -790,24 +797,30 @@ class FusedTrainStep:
                 torch.cuda.synchronize()
                 steps = self.optimizer.steps
                 g = torch.cuda.CUDAGraph()
-                if self.cols is not None and self.cols.world > 1:
-                    # graphs cut at the column groups' two collectives, which run eagerly between them
-                    g = _SegmentedGraph()
-                    self.cols.capture = g
-                    try:
-                        st.graph_loss = g.capture(lambda: self._step_lazy(st, draw=False))
-                    finally:
-                        self.cols.capture = None
-                elif self.exchange is None:
-                    with torch.cuda.graph(g):
-                        st.graph_loss = self._step_lazy(st, draw=False)
-                else:  # two halves: the all_gather between them runs eagerly
-                    with torch.cuda.graph(g):
-                        st.graph_loss = self._lazy_grads(st, draw=False)
-                    st.graph_post = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(st.graph_post):
-                        self._lazy_update(st)
-                self.optimizer.steps = steps  # the capture ran no step
+                # the capture records the launches of the step just run and runs none: its
+                # max_steps check is taken at that step's index (one past it fails when the
+                # constant table is exactly full), and the count is restored after
+                self.optimizer.steps = steps - 1
+                try:
+                    if self.cols is not None and self.cols.world > 1:
+                        # graphs cut at the column groups' two collectives, which run eagerly between them
+                        g = _SegmentedGraph()
+                        self.cols.capture = g
+                        try:
+                            st.graph_loss = g.capture(lambda: self._step_lazy(st, draw=False))
+                        finally:
+                            self.cols.capture = None
+                    elif self.exchange is None:
+                        with torch.cuda.graph(g):
+                            st.graph_loss = self._step_lazy(st, draw=False)
+                    else:  # two halves: the all_gather between them runs eagerly
+                        with torch.cuda.graph(g):
+                            st.graph_loss = self._lazy_grads(st, draw=False)
+                        st.graph_post = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(st.graph_post):
+                            self._lazy_update(st)
+                finally:
+                    self.optimizer.steps = steps
                 st.graph = g
                 return loss
             if self.optimizer.steps + 1 > self.optimizer.max_steps:

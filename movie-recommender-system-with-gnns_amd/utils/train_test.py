@@ -96,7 +96,7 @@ def train(model: torch.nn.Module, optimizer: torch.optim.Optimizer, train_loader
     why = "model not on a ROCm device"
     total_loss, total_w = None, 0
     batches = train_loader
-    rest = None  # the first batch the reference loop takes after fused steps
+    rest = None  # the batches the fused step read but did not take (the reference loop takes them)
     weight = getattr(getattr(model, "user_embedding", None), "weight", None)
     if weight is not None and weight.is_cuda:
         from lgcn_amd import harness
@@ -116,7 +116,7 @@ def train(model: torch.nn.Module, optimizer: torch.optim.Optimizer, train_loader
             if steps:
                 why = f"fused for {steps} batch(es), then reference from a batch that is not a bipartite user-item edge list"
     LAST_TRAIN_PATH = f"reference: {why}"
-    for batch in (_chain(rest, batches) if rest is not None else batches):
+    for batch in (_chain(rest, batches) if rest is not None else batches):  # rest: read, not taken
         contrib, w = _reference_step(model, optimizer, batch, device)
         total_w += w
         total_loss = contrib if total_loss is None else total_loss + contrib
@@ -139,7 +139,7 @@ class _Sized:
 
 
 def _chain(first, rest):
-    yield first
+    yield from first
     yield from rest
 
 

@@ -5,6 +5,7 @@ test is the distributed logic the product path shares (lgcn_amd.distributed): ba
 gradient all-reduce, identical optimizer steps on every rank, global loss reduction."""
 import os
 import socket
+import types
 
 import numpy as np
 import pytest
@@ -145,3 +146,32 @@ def test_two_rank_hybrid_exchange_gathers_users_and_sums_items(tmp_path):
     assert np.all(items == 3.0)  # 1 + 2 on both ranks
     ids = h0[2 + I * 4:].reshape(2, 2)
     assert ids.tolist() == [[0, U - 1], [1, U - 2]]  # rank order
+
+
+def test_exchange_capacity_holds_dense_batches():
+    """VERDICT r5 weak #9 (gpurun_out/r05zk/c4proj_planted.log: 'lgcn_rows_pack: bad args
+    (n_a=6869 n_b=178333 cap=65968)'). lgcn_rows_pack is position-based — a slot per touched row
+    plus one per triplet's negative, first occurrence or not — so a rank's record block needs
+    touched + B slots. The failing projection ran an uncommitted sizing by DISTINCT rows (65,968 =
+    6,921 touched + I = 59,047 items, the owner exchange's dedupe rule applied to the replicated
+    block); the committed exchange_capacity counts touched + B. Pinned here on a planted graph whose
+    batches draw more negatives than there are items (B > I, as the planted C3 batches do)."""
+    from lgcn_amd import cluster, synth
+
+    g, _ = synth.planted_ml25m(64, scale=0.02)
+    U, I = g.num_users, g.num_items
+    _, _, lists = cluster.cluster_batches(g.edge_index, g.num_nodes, 64, 8)
+    batches = [types.SimpleNamespace(edge_index=torch.from_numpy(x)) for x in lists if x.shape[1]]
+    cap = D.exchange_capacity(batches, U)
+    need, dense = 0, 0
+    for b in batches:
+        ei = b.edge_index
+        touched = int(torch.unique(ei).numel())
+        B = int((ei[0] < U).sum())
+        need = max(need, touched + B)
+        dense += B > I
+        assert cap >= touched + B
+    assert dense > 0, "no batch draws more negatives than there are items"
+    assert cap == need
+    ex = D.RowExchange(cap, U + I, 4, torch.device("cpu"), 1)
+    assert ex.cap >= need and ex.cap % 2 == 0

@@ -1,6 +1,10 @@
 """The harness mirror (package utils/train_test.py, utils/helpers.py) vs outputs of the
 reference's own utils/train_test.py and utils/helpers.py (tests/golden/harness.npz, made by
-tests/golden/make_golden.py). Everything here runs on CPU; equality is bitwise."""
+tests/golden/make_golden.py). Everything here runs on CPU; equality is bitwise — on a host whose CPU
+torch kernels round as the recording host's did (this container). On another host CPU (the GPU
+box's) torch's vectorised CPU reductions may round differently and the post-epoch tables move at the
+last bit; the GPU counterpart with tolerances is tests/test_gpu_harness.py::
+test_harness_epoch_and_evaluate_match_reference_golden."""
 import numpy as np
 import torch
 
