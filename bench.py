@@ -434,6 +434,175 @@ def settle_warmup(step, torch, dist=None, dev=None) -> dict:
         prev = ms
 
 
+def collective_fn(dist, torch, op: str, nbytes: int, group, n: int, dev):
+    """(fn, buffer bytes): one `op` over `group` (n ranks) of about nbytes (the whole buffer: the
+    all_reduce's tensor, reduce_scatter's / all_to_all's input, all_gather's output), fp32."""
+    m = max(1, -(-int(nbytes) // (4 * n)))  # floats per rank slice
+    f = dict(dtype=torch.float32, device=dev)
+    if op == "all_reduce":
+        buf = torch.zeros(n * m, **f)
+        return (lambda: dist.all_reduce(buf, group=group)), 4 * n * m
+    if op == "reduce_scatter":
+        inp, out = torch.zeros(n * m, **f), torch.empty(m, **f)
+        return (lambda: dist.reduce_scatter_tensor(out, inp, group=group)), 4 * n * m
+    if op == "all_gather":
+        inp, out = torch.zeros(m, **f), torch.empty(n * m, **f)
+        return (lambda: dist.all_gather_into_tensor(out, inp, group=group)), 4 * n * m
+    if op == "all_to_all":
+        inp, out = torch.zeros(n * m, **f), torch.empty(n * m, **f)
+        return (lambda: dist.all_to_all_single(out, inp, group=group)), 4 * n * m
+    raise ValueError(f"unknown collective {op!r}")
+
+
+def probe_collectives(dist, torch, dev, specs, reps: int = 10, sync=None) -> list:
+    """Untimed by the bench line: each spec {name, op, bytes, group, ranks} — a collective the
+    multi-GPU step or its projection (tools/project_scale.py, tools/project_c4.py) prices — run
+    2 + reps times on this node's ranks (all column groups at once, as in the step); ms is the
+    mean per call, the max over ranks; bus bandwidth by the rccl-tests convention
+    (tools/scale_model.BUS_FACTOR). A collective that raises on any rank is recorded as failed on
+    every rank (one all_reduce of [ms, failed] per spec)."""
+    from tools.scale_model import bus_gbps
+
+    sync = sync or (lambda: torch.cuda.synchronize())
+    out = []
+    for sp in specs:
+        rec = {"name": sp["name"], "op": sp["op"], "ranks": int(sp["ranks"]), "bytes": int(sp["bytes"])}
+        ms, failed = 0.0, 0.0
+        try:
+            fn, rec["bytes"] = collective_fn(dist, torch, sp["op"], sp["bytes"], sp.get("group"), sp["ranks"], dev)
+            for _ in range(2):
+                fn()
+            sync()
+            dist.barrier()
+            t = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            sync()
+            ms = (time.perf_counter() - t) / reps * 1e3
+        except Exception as e:  # noqa: BLE001 — recorded, agreed on
+            failed = 1.0
+            rec["error"] = f"{type(e).__name__}: {e}"[:160]
+            sync()
+        agree = torch.tensor([ms, failed], dtype=torch.float64, device=dev)
+        dist.all_reduce(agree, op=dist.ReduceOp.MAX)
+        ms, failed = float(agree[0].item()), bool(agree[1].item())
+        if failed:
+            rec.update(ms=None, busbw_GBps=None, algbw_GBps=None, failed=True)
+        else:
+            rec.update(ms=float(f"{ms:.5g}"), busbw_GBps=float(f"{bus_gbps(sp['op'], rec['bytes'], rec['ranks'], ms):.4g}"),
+                       algbw_GBps=float(f"{rec['bytes'] / (ms * 1e-3) / 1e9:.4g}"))
+        out.append(rec)
+    return out
+
+
+def project_chosen_grid(st, K: int, collectives: list, measured_ms: float, torch, dist) -> dict:
+    """projected_ms_per_step of the chosen C2 grid beside the measured one: the rank's own pieces
+    (partial pass, user pass, their pair launch; HIP events, untimed) and the collectives just
+    timed on this node, through tools/scale_model.simulate (the model tools/project_scale.py
+    prices with assumed bandwidths). The max over ranks of each piece."""
+    mode = str(st.get("mode"))
+    grid = st["grid"]
+    if not mode.startswith("reduce"):
+        return {"grid": f"{grid.R}x{grid.F}", "mode": st.get("mode"), "measured_ms_per_step": measured_ms,
+                "projected_ms_per_step": None,
+                "note": "no reduce exchange: the step is the rank's compute (its trial time)"}
+    from tools.scale_model import simulate
+
+    from lgcn_amd import _ffi
+
+    rplan = st["splan"]
+    x0u, x0i = st["x0"]
+    d = x0u.shape[1]
+    dev = x0u.device
+    part = torch.zeros((rplan.I_pad, d), device=dev)
+    acc = (torch.zeros((x0u.shape[0], d), device=dev), torch.zeros((x0i.shape[0], d), device=dev), x0u.shape[0])
+    y = torch.empty((x0u.shape[0], d), device=dev)
+
+    def timed(fn, reps=20):
+        for _ in range(3):
+            fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
+
+    with torch.no_grad():
+        t = torch.tensor([timed(lambda: rplan.run_partial(x0u, part)),
+                          timed(lambda: rplan.run_users(x0i, None, acc, y, _ffi.EPI_ADD, 1.0, 1.0)),
+                          timed(lambda: rplan.run_pair(x0u, part, x0i, None, acc, y, _ffi.EPI_ADD, 1.0, 1.0))],
+                         dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_p, t_u, t_pair = (float(v) for v in t.tolist())
+    by = {c["name"]: c for c in collectives}
+    key = f"{grid.R}x{grid.F}_items_"
+    if "a2a" in mode:  # all_to_all + ordered sums + all_gather; the last layer stops after the sums
+        parts = [by.get(key + "all_to_all"), by.get(key + "all_gather")]
+        t_ar = sum(c["ms"] for c in parts) if all(c and c["ms"] is not None for c in parts) else None
+        t_rs = parts[0]["ms"] if parts[0] and parts[0]["ms"] is not None else None
+    else:
+        ar, rs = by.get(key + "all_reduce"), by.get(key + "reduce_scatter")
+        t_ar = ar["ms"] if ar and ar["ms"] is not None else None
+        t_rs = rs["ms"] if rs and rs["ms"] is not None else None
+    out = {"grid": f"{grid.R}x{grid.F}", "mode": mode, "measured_ms_per_step": measured_ms,
+           "pieces_ms": {"partial_pass": t_p, "user_pass": t_u, "pair": t_pair},
+           "collective_ms": {"all_reduce_like": t_ar, "reduce_scatter_like": t_rs},
+           "compute_alone_ms": K * ((t_pair) if mode.endswith("fused") else (t_p + t_u))}
+    if t_ar is None or t_rs is None:
+        out["projected_ms_per_step"] = None
+        out["note"] = "a priced collective failed on this node"
+        return out
+    out["projected_ms_per_step"] = simulate(K, t_p, t_u, t_pair, t_ar, t_rs, mode.endswith("fused"))
+    out["measured_over_projected"] = measured_ms / out["projected_ms_per_step"]
+    return out
+
+
+def c2_collective_specs(world: int, d_full: int, num_items: int, groups: dict, candidates) -> list:
+    """The collectives the C2 reduce grids exchange (lgcn_amd.sharded.ItemReducer): per R > 1
+    grid, its column group's item partial table (I x d/F fp32) all-reduced K-1 times and
+    reduce-scattered once per step (ring), or all_to_all'd + all_gathered (a2a); and the
+    latency of a tiny all_reduce in the group and in the world."""
+    specs, seen = [], set()
+    for R, F, mode in candidates:
+        if R == 1 or (R, F) in seen or not str(mode).startswith("reduce"):
+            continue
+        seen.add((R, F))
+        nb = num_items * (d_full // F) * 4
+        g = groups.get((R, F))
+        for op in ("all_reduce", "reduce_scatter", "all_to_all", "all_gather"):
+            specs.append(dict(name=f"{R}x{F}_items_{op}", op=op, bytes=nb, group=g, ranks=R))
+        specs.append(dict(name=f"{R}x{F}_latency_all_reduce_8B", op="all_reduce", bytes=8, group=g, ranks=R))
+    specs.append(dict(name=f"world_latency_all_reduce_8B", op="all_reduce", bytes=8, group=None, ranks=world))
+    return specs
+
+
+def c4_collective_specs(world: int, dp_mode: str, exchange, cols, num_items: int, d: int, max_b: int) -> list:
+    """The collectives a C4 training step exchanges in the chosen mode (tools/project_c4.py prices
+    them): owner — the gradient blocks' and the replies' all_to_alls and the clip partials'
+    all_gather; hybrid — the item gradient table's all_reduce and the users' record all_gather;
+    replicated — the record blocks' all_gather; columns — the triplets' [B, 6] all_reduce. Plus a
+    tiny all_reduce's latency."""
+    specs = []
+    if dp_mode == "owner" and exchange is not None:
+        specs += [dict(name="owner_blocks_all_to_all", op="all_to_all", bytes=exchange.send.numel() * 4),
+                  dict(name="owner_replies_all_to_all", op="all_to_all", bytes=exchange.reply_send.numel() * 4),
+                  dict(name="owner_norm_all_gather", op="all_gather", bytes=exchange.partials_all.numel() * 4)]
+    elif dp_mode == "hybrid" and exchange is not None:
+        specs += [dict(name="hybrid_items_all_reduce", op="all_reduce", bytes=num_items * d * 4),
+                  dict(name="hybrid_users_all_gather", op="all_gather", bytes=world * exchange.blk * 4)]
+    elif exchange is not None:
+        specs += [dict(name="records_all_gather", op="all_gather", bytes=world * exchange.blk * 4)]
+    if cols is not None:
+        specs += [dict(name="columns_bpr_sums_all_reduce", op="all_reduce", bytes=6 * max_b * 4)]
+    specs.append(dict(name="world_latency_all_reduce_8B", op="all_reduce", bytes=8))
+    for sp in specs:
+        sp.update(group=None, ranks=world)
+    return specs
+
+
 def schedule_traffic(sched, n_src_rows: int, d: int):
     """(compulsory bytes of one middle layer's item pass over `sched`, its launches, edges, rows
     finished in the pass): every source
@@ -613,7 +782,8 @@ def main():
                 x0u, x0i = user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous()
                 fused = mode.endswith("fused")
                 return dict(grid=grid, shards=ushards, splan=rplan, scheds=[rplan.users, rplan.partial], ex=red,
-                            mode=mode, step=lambda: propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused))
+                            mode=mode, x0=(x0u, x0i),
+                            step=lambda: propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused))
             shards = RowShards.build(in_deg, U, grid.R)
             splan = ShardedPlan(ei, shards, grid.row_group, c1 - c0, chunk)
             x0p = shards.to_padded(user_w[:, c0:c1].contiguous(), item_w[:, c0:c1].contiguous())
@@ -635,6 +805,17 @@ def main():
                 torch.cuda.synchronize()
             return (time.perf_counter() - t) / n * 1e3
 
+        # the collectives the reduce grids price, timed once on this node before any trial (untimed
+        # by the bench line): the first node run checks tools/project_scale.py's assumptions
+        cands = ([tuple(int(v) for v in args.shard.split("x")) + (args.exchange_mode,)] if args.shard else
+                 grid_candidates(world, d_full, p2p=os.environ.get("LGCN_GRID_NO_P2P") != "1"))
+        for R, F, _ in cands:  # every rank creates every column group, in one order
+            if R > 1 and (R, F) not in groups:
+                groups[(R, F)] = ShardGrid.build(world, rank, d_full, R, F).exchange_group(dist)
+        collectives = probe_collectives(dist, torch, dev, c2_collective_specs(world, d_full, I, groups, cands))
+        for c in collectives:
+            log(f"[rank {rank}] collective {c['name']}: {c['bytes'] / 1e6:.3f} MB over {c['ranks']} ranks, "
+                f"{c['ms']} ms, bus {c['busbw_GBps']} GB/s")
         if args.shard:
             R, F = (int(v) for v in args.shard.split("x"))
             st = build_grid(R, F, args.exchange_mode)
@@ -853,6 +1034,9 @@ def main():
         result["config"]["tuning"] = args.tuned  # the source-sliced schedule's hub chunk
     if grid_trials is not None:
         result["config"]["grid_trials_ms_per_step"] = grid_trials
+    if sharded:
+        result["collectives"] = collectives
+        result["projection"] = project_chosen_grid(st, K, collectives, elapsed / args.steps * 1e3, torch, dist)
     if step_ev is not None:
         series = [round(a.elapsed_time(b), 5) for a, b in zip(step_ev, step_ev[1:])]
         result["step_ms"] = series
@@ -1056,6 +1240,12 @@ def run_train(args):
                                lazy=lazy, exchange=exchange, cols=cols,
                                neg_seed=(7 if cols is not None else 1000 + rank) if dp_mode != "replicated" else None)
 
+    collectives = None
+    if world > 1:  # what this mode exchanges, timed on the node before the warm-up (untimed)
+        max_b = max(int((b.edge_index[0] < U).sum()) for b in batches)
+        collectives = probe_collectives(dist, torch, dev, c4_collective_specs(world, dp_mode, exchange, cols, I, d,
+                                                                              max_b))
+
     def step(bidx, nxt=None):
         batch = batches[bidx]
         if fused is not None:
@@ -1150,6 +1340,8 @@ def run_train(args):
         result["config"]["tuning"] = args.tuned
     if exchange is not None and hasattr(exchange, "bytes"):
         result["exchange"] = {"mode": dp_mode, "MB_received_per_rank_per_step": exchange.bytes / args.steps / 1e6}
+    if collectives is not None:
+        result["collectives"] = collectives
     if world == 1 and not args.no_harness:
         # what a user of the reference harness gets: utils.train_test.train() over one epoch of the
         # same batches with the reference's torch Adam(1e-3) (clip 1 inside), routed to the fused

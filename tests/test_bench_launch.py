@@ -167,3 +167,61 @@ def test_launch_fallback_without_p2p(monkeypatch, first_rc, first_out, kw, relau
     rc = b.launch_with_fallback(_args(**kw), launch=fake_launch)
     assert calls == ([None, "1"] if relaunched else [None])
     assert rc == (0 if relaunched else first_rc)
+
+
+def _collectives_worker(rank, world, port, out):
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path[:0] = [str(ROOT), str(ROOT / "movie-recommender-system-with-gnns_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b = _bench()
+    cpu = torch.device("cpu")
+    # the C2 4x2-shaped specs at world 2: one 1 x 2 "grid" has no exchange, so price a 2 x 1 group
+    specs = b.c2_collective_specs(world, 64, 3000, {(2, 1): None}, [(2, 1, "reduce"), (1, 2, None)])
+    specs += b.c4_collective_specs(world, "hybrid", type("X", (), {"blk": 1000})(), None, 3000, 8, 500)
+    rec = b.probe_collectives(dist, torch, cpu, specs, reps=3, sync=lambda: None)
+    if rank == 0:
+        with open(out, "w") as f:
+            json.dump(rec, f)
+    dist.destroy_process_group()
+
+
+def test_collectives_probe_schema(tmp_path):
+    """bench.py --gpus N times the collectives its projections price (untimed,
+    before the grid trials / the training warm-up) and writes them into the JSON line: name, op,
+    ranks, bytes, ms (max over ranks), bus and algorithm bandwidth; a collective the backend lacks
+    is recorded as failed on every rank instead of ending the run. World-2 gloo rehearsal."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "coll.json")
+    mp.spawn(_collectives_worker, args=(2, port, out), nprocs=2, join=True)
+    with open(out) as f:
+        rec = json.load(f)
+    names = [r["name"] for r in rec]
+    assert names == ["2x1_items_all_reduce", "2x1_items_reduce_scatter", "2x1_items_all_to_all", "2x1_items_all_gather",
+                     "2x1_latency_all_reduce_8B", "world_latency_all_reduce_8B", "hybrid_items_all_reduce",
+                     "hybrid_users_all_gather", "world_latency_all_reduce_8B"]
+    for r in rec:
+        assert set(r) >= {"name", "op", "ranks", "bytes", "ms", "busbw_GBps", "algbw_GBps"}, r
+        assert r["ranks"] == 2 and r["bytes"] >= 8
+        if r.get("failed"):
+            assert r["ms"] is None and r["busbw_GBps"] is None
+        else:
+            assert r["ms"] > 0 and r["busbw_GBps"] > 0
+    by = {r["name"]: r for r in rec}
+    assert not by["2x1_items_all_reduce"].get("failed")  # gloo has all_reduce
+    assert by["2x1_items_all_reduce"]["bytes"] == 3000 * 64 * 4
+    # all_reduce's bus bytes: 2 (n-1)/n of the buffer
+    r = by["2x1_items_all_reduce"]
+    assert abs(r["busbw_GBps"] - r["algbw_GBps"]) <= 0.02 * r["algbw_GBps"] + 0.01

@@ -35,6 +35,9 @@ sys.path.insert(0, os.path.join(ROOT, "movie-recommender-system-with-gnns_amd"))
 from lgcn_amd import _ffi, synth  # noqa: E402
 from lgcn_amd.sharded import ReducePlan, ShardGrid, UserShards  # noqa: E402
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from scale_model import simulate  # noqa: E402,F401  (the shared event model)
+
 
 def timed(fn, reps=30):
     """mean ms of fn() over reps (events on the current stream, after 3 warm-ups)."""
@@ -63,24 +66,6 @@ def pieces(rplan, x0u, x0i, d):
     t_u = timed(lambda: rplan.run_users(x0i, None, acc, y, _ffi.EPI_ADD, 1.0, 1.0))
     t_pair = timed(lambda: rplan.run_pair(x0u, part, x0i, None, acc, y, _ffi.EPI_ADD, 1.0, 1.0))
     return t_p, t_u, t_pair
-
-
-def simulate(K, t_p, t_u, t_pair, t_ar, t_rs, fused):
-    """ms per K-layer step of one rank (compute on one stream, the collectives serialised on
-    another); the final stack mean (a few us) is ignored."""
-    if fused:
-        t, ar_done = 0.0, 0.0
-        for k in range(1, K + 1):
-            t = max(t, ar_done) + t_pair
-            ar_done = t + (t_ar if k < K else t_rs)
-        return ar_done
-    t, comm, ar_done = 0.0, 0.0, {0: 0.0}
-    for k in range(1, K + 1):
-        t += t_p  # P_k needs U_{k-1}: the compute stream is in order
-        comm = max(comm, t) + (t_ar if k < K else t_rs)
-        ar_done[k] = comm
-        t = max(t, ar_done[k - 1]) + t_u  # U_k reads the items reduced one layer earlier
-    return max(t, ar_done[K])
 
 
 def simulate_chunked(K, t_p, t_u, t_ar, t_rs, blocks, lat, t_block=0.0):
