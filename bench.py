@@ -1119,8 +1119,9 @@ def harness_times(batches, U, I, K, d, dev, epochs=2):
     out["note"] = ("utils.train_test.train() per step over one epoch of the bench's batches (the second of two), "
                    "torch.optim.Adam(lr=1e-3) + clip 1, loss read once per epoch; includes the epoch-end flush; "
                    "fused_fresh_*_tensors: the loader yields a new edge_index per batch every epoch, as the "
-                   "reference's PyG DataLoader does (each batch's state found by an XXH3 digest of its bytes; a "
-                   "device tensor is copied to the host for it, one sync per batch)")
+                   "reference's PyG DataLoader does (each batch's state found by a digest of its bytes: XXH3 on the "
+                   "host for a host tensor; for a device tensor lgcn_digest128 on a side stream, started one "
+                   "batch ahead, no sync per batch)")
     return out
 
 

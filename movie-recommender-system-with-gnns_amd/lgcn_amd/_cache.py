@@ -42,42 +42,74 @@ except ImportError:  # pragma: no cover - xxhash ships with the image
 
 
 class _PendingDigest:
-    """A device digest in flight: 16 bytes landing in pinned host memory behind an event."""
+    """A device digest in flight: 16 bytes landing in a pinned host slot behind an event."""
 
-    __slots__ = ("host", "event", "keep")
+    __slots__ = ("ring", "slot", "value")
 
-    def __init__(self, host, event, keep):
-        self.host, self.event, self.keep = host, event, keep
+    def __init__(self, ring, slot):
+        self.ring, self.slot, self.value = ring, slot, None
 
     def result(self) -> bytes:
-        self.event.synchronize()
-        self.keep = None
-        return self.host.numpy().tobytes()
+        if self.value is None:
+            ring, s = self.ring, self.slot
+            ring.events[s].synchronize()
+            self.value = ring.host[s].numpy().tobytes()
+            if ring.owner[s] is self:
+                ring.owner[s] = None
+        return self.value
 
 
-# per device: the digest's workspace (uint64[2 * LGCN_DIGEST_BLOCKS])
-_DIGEST_WS: dict = {}
+class _DigestRing:
+    """Per device: the digests' side stream, workspace and a ring of (device out, pinned host slot,
+    event) — preallocated, so a digest costs two launches, one copy and one event record on the
+    host (no allocation). A slot still owned by an uncollected digest is collected before reuse."""
+
+    SLOTS = 16
+
+    def __init__(self, dev):
+        from . import _ffi
+
+        self.stream = torch.cuda.Stream(dev)
+        self.ws = torch.empty(2 * _ffi.DIGEST_BLOCKS, dtype=torch.int64, device=dev)
+        self.out = torch.empty((self.SLOTS, 2), dtype=torch.int64, device=dev)
+        self.host = torch.empty((self.SLOTS, 2), dtype=torch.int64, pin_memory=True)
+        self.events = [torch.cuda.Event() for _ in range(self.SLOTS)]
+        self.owner = [None] * self.SLOTS
+        self.next = 0
+
+
+_DIGEST_RINGS: dict = {}
 
 
 def _device_digest_start(t: torch.Tensor) -> _PendingDigest:
-    """lgcn_digest128 of a device tensor's bytes on its device's current stream; no wait."""
+    """lgcn_digest128 of a device tensor's bytes, enqueued on a side stream that waits for the
+    current stream's work so far (the tensor's producer) — the current stream goes on with the
+    caller's work (a training step) while the digest runs beside it; no host wait."""
     from . import _ffi
 
     lib = _ffi.load()
-    c = t.detach().contiguous()
-    dev = c.device
-    ws = _DIGEST_WS.get(dev)
-    if ws is None:
-        ws = _DIGEST_WS[dev] = torch.empty(2 * _ffi.DIGEST_BLOCKS, dtype=torch.int64, device=dev)
-    out = torch.empty(2, dtype=torch.int64, device=dev)
-    nbytes = c.numel() * c.element_size()
-    _ffi.check(lib.lgcn_digest128(c.data_ptr() if nbytes else None, nbytes, ws.data_ptr(), ws.numel(),
-                                  out.data_ptr(), _ffi.stream_of(dev)), "lgcn_digest128")
-    host = torch.empty(2, dtype=torch.int64, pin_memory=True)
-    host.copy_(out, non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
-    return _PendingDigest(host, ev, (c, out))
+    dev = t.device
+    ring = _DIGEST_RINGS.get(dev)
+    if ring is None:
+        ring = _DIGEST_RINGS[dev] = _DigestRing(dev)
+    s = ring.next
+    ring.next = (s + 1) % ring.SLOTS
+    if ring.owner[s] is not None:  # an uncollected digest still owns the slot: collect it first
+        ring.owner[s].result()
+    stream = ring.stream
+    stream.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(stream):
+        c = t.detach().contiguous()
+        nbytes = c.numel() * c.element_size()
+        _ffi.check(lib.lgcn_digest128(c.data_ptr() if nbytes else None, nbytes, ring.ws.data_ptr(), ring.ws.numel(),
+                                      ring.out[s].data_ptr(), _ffi.stream_of(dev)), "lgcn_digest128")
+        ring.host[s].copy_(ring.out[s], non_blocking=True)
+        ring.events[s].record(stream)
+    # the caching allocator must not hand the tensor's blocks out again before the side stream is done
+    c.record_stream(stream)
+    p = _PendingDigest(ring, s)
+    ring.owner[s] = p
+    return p
 
 
 def _key_parts(t: torch.Tensor) -> tuple:

@@ -46,7 +46,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--chunk", type=int, default=256)
     ap.add_argument("--orders", default="overlapped,fused,fused-seq")
+    ap.add_argument("--rank-chunk", type=int, default=0, help="override lgcn_amd.plan.RANK_CHUNK (0: keep)")
     args = ap.parse_args()
+    if args.rank_chunk:
+        from lgcn_amd import plan as _plan
+
+        _plan.RANK_CHUNK = args.rank_chunk
     dev = torch.device("cuda")
     g = synth.ml25m_shaped(seed=0)
     U, I, N = g.num_users, g.num_items, g.num_nodes
