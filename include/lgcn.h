@@ -410,15 +410,6 @@ int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split,
                    const int64_t* u, const int64_t* p, const int64_t* n, int64_t B, int32_t d,
                    const uint8_t* touched, float div, float mul,
                    float coeff, float* cf, float* cw, float* terms, lgcn_stream_t stream);
-/* lgcn_bpr_fused without the negatives' dF rows (ABI 9): cf's rows [2B, 3B) are not written; nsc
- * (device float[B, 4], 16-byte aligned) gets each triplet's (dcn, cn, 1/|u|, 1/|n|) instead, from
- * which lgcn_sorted_scatter_add_bpr recomputes those rows bitwise (the same float operations) —
- * 16 bytes per triplet written instead of 4d. */
-int lgcn_bpr_fused_neg(const float* f_lo, const float* f_hi, int64_t f_split,
-                       const float* w_lo, const float* w_hi, int64_t w_split, int64_t U,
-                       const int64_t* u, const int64_t* p, const int64_t* n, int64_t B, int32_t d,
-                       const uint8_t* touched, float div, float mul,
-                       float coeff, float* cf, float* cw, float* terms, float* nsc, lgcn_stream_t stream);
 /* Column-sharded form (exact single-GPU training split over ranks by embedding columns, SURVEY
  * §8e's parity-preserving alternative): the rows are one rank's d of d_full columns.
  *   phase 1: sums[b*6 + k] = this rank's partial of (|u|^2, |p|^2, |n|^2, u.p, u.n, reg squares)
@@ -488,17 +479,6 @@ int lgcn_sorted_scatter_add(const int64_t* rowptr, const int32_t* perm, int64_t 
                             float div, const float* C2, const float* reg_w_lo, const float* reg_w_hi,
                             int64_t reg_w_split, float reg_coeff, int64_t reg_B, float* c2buf, uint8_t* c2flag,
                             const uint8_t* store_unless, lgcn_stream_t stream);
-/* lgcn_sorted_scatter_add (no C2 / reg parking) with the C rows recomputed from
- * lgcn_bpr_fused_neg's scalars (ABI 9): row b = dcn_b * (u_c / |u_b| - cn_b * n_c / |n_b|) / |n_b|
- * per column, on the rows lgcn_bpr_fused read (f, or (w / bpr_div) * bpr_mul where touched[r] == 0;
- * u: the triplets' user rows) — bitwise the materialised rows, so bitwise lgcn_sorted_scatter_add's
- * result; the [B, d] table is neither written nor read. */
-int lgcn_sorted_scatter_add_bpr(const int64_t* rowptr, const int32_t* perm, int64_t nrows, int64_t key_offset,
-                                int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
-                                uint8_t* c2flag, const uint8_t* store_unless, const float* f_lo, const float* f_hi,
-                                int64_t f_split, const float* w_lo, const float* w_hi, int64_t w_split,
-                                const int64_t* u, const float* nsc, const uint8_t* touched, float bpr_div,
-                                float bpr_mul, lgcn_stream_t stream);
 /* The fixed (user, positive) reg-gradient rows of a batch: rowptr counts the contributions per
  * row (a segment plan of the 2B keys); every listed row with n > 0 gets out[r] += n copies of
  * kreg * W[r] added in sequence (kreg as in lgcn_range_scatter_add). rows (device int32[n_rows],

@@ -92,9 +92,6 @@ struct BprArgs {
     // column-sharded training (lgcn_bpr_fused_cols): the rows are one rank's d of d_full columns
     float* sums;     // [B, 6] per-triplet (|u|^2, |p|^2, |n|^2, u.p, u.n, reg squares)
     int32_t d_full;  // the full width (reg mean); == d unsharded
-    // nullable [B, 4]: the negatives' scalars (dcn, cn, 1/|u|, 1/|n|) instead of their dF rows
-    // (lgcn_bpr_fused_neg: the sorted scatter recomputes each row from them, NegSrc)
-    float* nsc;
 };
 
 // phase 0: fused (the sums reduced inside the lane group); 1: write this rank's column partials
@@ -192,7 +189,7 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
 #undef LGCN_BPR_LANE
         cfu[k * LPR] = du;
         cfp[k * LPR] = dp;
-        if (a.nsc == nullptr) cfn[k * LPR] = dn;
+        cfn[k * LPR] = dn;
         if (a.cw != nullptr) {  // materialised reg rows (else the scatters form them, RegSrc)
             cwu[k * LPR] = make_float4(kreg * WU[k].x, kreg * WU[k].y, kreg * WU[k].z, kreg * WU[k].w);
             cwp[k * LPR] = make_float4(kreg * WP[k].x, kreg * WP[k].y, kreg * WP[k].z, kreg * WP[k].w);
@@ -202,7 +199,6 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
     if (l == 0) {
         a.terms[b] = sp;
         a.terms[a.B + b] = sreg;
-        if (a.nsc != nullptr) *reinterpret_cast<float4*>(a.nsc + 4 * b) = make_float4(dcn, cn, inu, inn);
     }
 }
 
@@ -563,119 +559,6 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
 // rowptr[nrows+1], perm[B] = b). One lane group per row: flags (1 at the row's first b), the C and
 // C2 sums in b order — the range scatter's association, so bitwise its result — the parked C2
 // sum, and the (sum * mul) / div store or add.
-// The negatives' dF rows recomputed from lgcn_bpr_fused_neg's per-triplet scalars instead of read
-// from a [B, d] table: row b is dcn * (u_c / |u| - cn * n_c / |n|) / |n| per column, the SAME float
-// operations in the same order as k_bpr_fused's (dn.c = dcn * (av - cn * cv) * inn, av = u_c * inu,
-// cv = n_c * inn), on the same u / n rows (F, or (W / div) * mul where the batch never reached the
-// row) — so every sum is bitwise the materialised table's.
-struct NegSrc {
-    const float* f_lo;
-    const float* f_hi;
-    int64_t f_split;
-    const float* w_lo;
-    const float* w_hi;
-    int64_t w_split;
-    const int64_t* u;         // [B] the triplets' user rows
-    const float* nsc;         // [B, 4] (dcn, cn, 1/|u|, 1/|n|)
-    const uint8_t* touched;   // nullable
-    float div;
-    float mul;
-};
-
-template <int LPR, int NV>
-__device__ __forceinline__ void bpr_row(const NegSrc& s, int64_t r, int64_t d, int l, float4 (&x)[NV]) {
-    const bool t = s.touched == nullptr || s.touched[r];
-    const float4* p = reinterpret_cast<const float4*>(t ? srow(s.f_lo, s.f_hi, s.f_split, r, d)
-                                                        : srow(s.w_lo, s.w_hi, s.w_split, r, d)) + l;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        x[k] = p[k * LPR];
-        if (!t) x[k] = make_float4((x[k].x / s.div) * s.mul, (x[k].y / s.div) * s.mul, (x[k].z / s.div) * s.mul,
-                                   (x[k].w / s.div) * s.mul);
-    }
-}
-
-__device__ __forceinline__ float neg_lane(float dcn, float cn, float inu, float inn, float uc, float nc) {
-    const float av = uc * inu, cv = nc * inn;
-    return dcn * (av - cn * cv) * inn;
-}
-
-template <int LPR, int NV>
-__device__ __forceinline__ float4 neg_row_k(float4 sc, const float4& u, const float4& n) {
-    return make_float4(neg_lane(sc.x, sc.y, sc.z, sc.w, u.x, n.x), neg_lane(sc.x, sc.y, sc.z, sc.w, u.y, n.y),
-                       neg_lane(sc.x, sc.y, sc.z, sc.w, u.z, n.z), neg_lane(sc.x, sc.y, sc.z, sc.w, u.w, n.w));
-}
-
-// k_sorted_scatter with the C rows recomputed (NegSrc; no C2 / reg parking: the sorted path's
-// reg rows come from lgcn_grouped_reg_add): the row's own F / W row loaded once, then per
-// contribution its user's row and scalars, four at a time, added in b order.
-template <int LPR, int NV>
-__global__ __launch_bounds__(kBlock) void k_sorted_scatter_bpr(const int64_t* __restrict__ rowptr,
-                                                               const int32_t* __restrict__ perm, int64_t nrows,
-                                                               int64_t key_offset, int32_t d, float* out_lo,
-                                                               float* out_hi, int64_t split, float mul, float div,
-                                                               uint8_t* __restrict__ c2flag,
-                                                               const uint8_t* __restrict__ store_unless, NegSrc ns) {
-    constexpr int GPB = kBlock / LPR;
-    const int g = threadIdx.x / LPR;
-    const int l = threadIdx.x % LPR;
-    const int64_t r = int64_t(blockIdx.x) * GPB + g;
-    if (r >= nrows) return;
-    const int64_t q0 = rowptr[r], q1 = rowptr[r + 1];
-    if (q0 == q1) return;
-    if (c2flag)
-        for (int64_t q = q0 + l; q < q1; q += LPR) c2flag[perm[q]] = (q == q0) ? 1 : 0;
-    const int64_t row = r + key_offset;
-    float4 nr[NV];
-    bpr_row<LPR, NV>(ns, row, d, l, nr);
-    float4 acc[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4* nsc4 = reinterpret_cast<const float4*>(ns.nsc);
-    int64_t q = q0;
-    for (; q + 4 <= q1; q += 4) {
-        float4 sc[4], ur[4][NV];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int64_t b = perm[q + u];
-            sc[u] = nsc4[b];
-            bpr_row<LPR, NV>(ns, ns.u[b], d, l, ur[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int k = 0; k < NV; ++k) {
-                const float4 v = neg_row_k<LPR, NV>(sc[u], ur[u][k], nr[k]);
-                acc[k] = make_float4(acc[k].x + v.x, acc[k].y + v.y, acc[k].z + v.z, acc[k].w + v.w);
-            }
-    }
-    for (; q < q1; ++q) {
-        const int64_t b = perm[q];
-        const float4 sc = nsc4[b];
-        float4 ur[NV];
-        bpr_row<LPR, NV>(ns, ns.u[b], d, l, ur);
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-            const float4 v = neg_row_k<LPR, NV>(sc, ur[k], nr[k]);
-            acc[k] = make_float4(acc[k].x + v.x, acc[k].y + v.y, acc[k].z + v.z, acc[k].w + v.w);
-        }
-    }
-    float4* o = reinterpret_cast<float4*>(srow(out_lo, out_hi, split, row, int64_t(d))) + l;
-    if (store_unless && !store_unless[row]) {
-#pragma unroll
-        for (int k = 0; k < NV; ++k)
-            o[k * LPR] = make_float4((acc[k].x * mul) / div, (acc[k].y * mul) / div, (acc[k].z * mul) / div,
-                                     (acc[k].w * mul) / div);
-    } else {
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-            const float4 v = o[k * LPR];
-            o[k * LPR] = make_float4(v.x + (acc[k].x * mul) / div, v.y + (acc[k].y * mul) / div,
-                                     v.z + (acc[k].z * mul) / div, v.w + (acc[k].w * mul) / div);
-        }
-    }
-}
-
 template <int LPR, int NV>
 __global__ __launch_bounds__(kBlock) void k_sorted_scatter(const int64_t* __restrict__ rowptr,
                                                            const int32_t* __restrict__ perm, int64_t nrows,
@@ -813,17 +696,6 @@ int launch_ss(const int64_t* rowptr, const int32_t* perm, int64_t nrows, int64_t
     return check_launch("k_sorted_scatter");
 }
 
-template <int LPR, int NV>
-int launch_ssb(const int64_t* rowptr, const int32_t* perm, int64_t nrows, int64_t key_offset, int32_t d, float* lo,
-               float* hi, int64_t split, float mul, float div, uint8_t* c2flag, const uint8_t* store_unless,
-               const NegSrc& ns, hipStream_t s) {
-    constexpr int GPB = kBlock / LPR;
-    const int64_t blocks = (nrows + GPB - 1) / GPB;
-    k_sorted_scatter_bpr<LPR, NV><<<dim3(static_cast<unsigned>(blocks)), kBlock, 0, s>>>(
-        rowptr, perm, nrows, key_offset, d, lo, hi, split, mul, div, c2flag, store_unless, ns);
-    return check_launch("k_sorted_scatter_bpr");
-}
-
 // Rows of a segment plan (rowptr over N rows, n contributions to row r): out[r] += n copies of
 // kreg * W[r] summed in sequence — the fixed (user, positive) reg-gradient rows, added after the
 // backward (reference utils/train_test.py:38-41 through autograd), without a [2B, d] table.
@@ -956,23 +828,7 @@ int lgcn_bpr_fused(const float* f_lo, const float* f_hi, int64_t f_split, const 
         (cw && !al16(cw)))
         return fail(LGCN_E_UNSUPPORTED, "lgcn_bpr_fused: needs d %% 4 == 0 and 16-byte aligned rows (d=%d)", d);
     BprArgs a{f_lo, f_hi, f_split, w_lo, w_hi, w_split, U, u, p, n, B, d, touched, div, mul, coeff, cf, cw, terms,
-              nullptr, d, nullptr};
-    return bpr_dispatch(a, kBprFused, as_stream(stream));
-}
-
-int lgcn_bpr_fused_neg(const float* f_lo, const float* f_hi, int64_t f_split, const float* w_lo, const float* w_hi,
-                       int64_t w_split, int64_t U, const int64_t* u, const int64_t* p, const int64_t* n, int64_t B,
-                       int32_t d, const uint8_t* touched, float div, float mul, float coeff, float* cf, float* cw,
-                       float* terms, float* nsc, lgcn_stream_t stream) {
-    if (B < 0 || d <= 0 || U < 0) return fail(LGCN_E_ARG, "lgcn_bpr_fused_neg: bad sizes");
-    if (B == 0) return LGCN_OK;
-    if (!f_lo || !w_lo || !u || !p || !n || !cf || !terms || !nsc)
-        return fail(LGCN_E_ARG, "lgcn_bpr_fused_neg: null pointer");
-    if (d % 4 != 0 || !al16(f_lo) || !al16(w_lo) || (f_hi && !al16(f_hi)) || (w_hi && !al16(w_hi)) || !al16(cf) ||
-        (cw && !al16(cw)) || !al16(nsc))
-        return fail(LGCN_E_UNSUPPORTED, "lgcn_bpr_fused_neg: needs d %% 4 == 0 and 16-byte aligned rows (d=%d)", d);
-    BprArgs a{f_lo, f_hi, f_split, w_lo, w_hi, w_split, U, u, p, n, B, d, touched, div, mul, coeff, cf, cw, terms,
-              nullptr, d, nsc};
+              nullptr, d};
     return bpr_dispatch(a, kBprFused, as_stream(stream));
 }
 
@@ -989,7 +845,7 @@ int lgcn_bpr_fused_cols(const float* f_lo, const float* f_hi, int64_t f_split, c
         (cf && !al16(cf)) || (cw && !al16(cw)))
         return fail(LGCN_E_UNSUPPORTED, "lgcn_bpr_fused_cols: needs d %% 4 == 0 and 16-byte aligned rows (d=%d)", d);
     BprArgs a{f_lo, f_hi, f_split, w_lo, w_hi, w_split, U, u, p, n, B, d, touched, div, mul, coeff, cf, cw, terms,
-              sums, d_full, nullptr};
+              sums, d_full};
     return bpr_dispatch(a, phase, as_stream(stream));
 }
 
@@ -1045,34 +901,6 @@ int lgcn_sorted_scatter_add(const int64_t* rowptr, const int32_t* perm, int64_t 
         default: return fail(LGCN_E_UNSUPPORTED, "lgcn_sorted_scatter_add: d=%d", d);
     }
 #undef LGCN_SS
-}
-
-int lgcn_sorted_scatter_add_bpr(const int64_t* rowptr, const int32_t* perm, int64_t nrows, int64_t key_offset,
-                                int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
-                                uint8_t* c2flag, const uint8_t* store_unless, const float* f_lo, const float* f_hi,
-                                int64_t f_split, const float* w_lo, const float* w_hi, int64_t w_split,
-                                const int64_t* u, const float* nsc, const uint8_t* touched, float bpr_div,
-                                float bpr_mul, lgcn_stream_t stream) {
-    if (nrows < 0 || d <= 0 || (nrows > 0 && (!rowptr || !perm || !out_lo || !f_lo || !w_lo || !u || !nsc)))
-        return fail(LGCN_E_ARG, "lgcn_sorted_scatter_add_bpr: bad args");
-    if (nrows == 0) return LGCN_OK;
-    if (d % 4 != 0 || !al16(out_lo) || (out_hi && !al16(out_hi)) || !al16(f_lo) || (f_hi && !al16(f_hi)) ||
-        !al16(w_lo) || (w_hi && !al16(w_hi)) || !al16(nsc))
-        return fail(LGCN_E_UNSUPPORTED, "lgcn_sorted_scatter_add_bpr: needs d %% 4 == 0 and aligned rows");
-    hipStream_t s = as_stream(stream);
-    const NegSrc ns{f_lo, f_hi, f_split, w_lo, w_hi, w_split, u, nsc, touched, bpr_div, bpr_mul};
-#define LGCN_SSB(L, V) launch_ssb<L, V>(rowptr, perm, nrows, key_offset, d, out_lo, out_hi, split, mul, div, c2flag, store_unless, ns, s)
-    switch (d) {
-        case 8: return LGCN_SSB(2, 1);
-        case 16: return LGCN_SSB(4, 1);
-        case 32: return LGCN_SSB(8, 1);
-        case 64: return LGCN_SSB(16, 1);
-        case 128: return LGCN_SSB(32, 1);
-        case 256: return LGCN_SSB(64, 1);
-        case 512: return LGCN_SSB(64, 2);
-        default: return fail(LGCN_E_UNSUPPORTED, "lgcn_sorted_scatter_add_bpr: d=%d", d);
-    }
-#undef LGCN_SSB
 }
 
 int lgcn_grouped_reg_add(const int64_t* rowptr, int64_t nrows, int64_t key_offset, const float* w_lo,

@@ -83,8 +83,6 @@ _SIGS = {
     "lgcn_bpr_fused": ([_vp, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _f32, _f32, _f32, _vp, _vp,
                         _vp, _vp],
                        ctypes.c_int),
-    "lgcn_bpr_fused_neg": ([_vp, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _f32, _f32, _f32,
-                            _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_bpr_fused_cols": ([_vp, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _f32, _f32,
                              _f32, _vp, _i32, _vp, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_bpr_loss": ([_vp, _i64, _i32, _f32, _vp, _vp, _vp], ctypes.c_int),
@@ -96,8 +94,6 @@ _SIGS = {
                                     ctypes.c_int),
     "lgcn_sorted_scatter_add": ([_vp, _vp, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _i64,
                                  _f32, _i64, _vp, _vp, _vp, _vp], ctypes.c_int),
-    "lgcn_sorted_scatter_add_bpr": ([_vp, _vp, _i64, _i64, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp,
-                                     _i64, _vp, _vp, _i64, _vp, _vp, _vp, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_grouped_reg_add": ([_vp, _i64, _i64, _vp, _vp, _i64, _i32, _f32, _i64, _vp, _vp, _i64, _vp], ctypes.c_int),
     "lgcn_reg_rows_add": ([_vp, _vp, _i64, _vp, _vp, _i64, _i32, _f32, _i64, _vp, _vp, _i64, _vp], ctypes.c_int),
     "lgcn_adam_consts": ([_vp, _i64, _i64, _f32, ctypes.c_double, ctypes.c_double, _vp], ctypes.c_int),

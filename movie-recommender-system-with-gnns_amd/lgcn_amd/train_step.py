@@ -227,10 +227,6 @@ class _BatchState:
             self.c2buf = torch.empty((B if self.neg_rowptr is None else 1, d), dtype=torch.float32, device=dev)
             self.c2flag = torch.empty(B, dtype=torch.uint8, device=dev)
             self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
-        # sorted path: the negatives' dF rows are recomputed by the scatter from 4 scalars per
-        # triplet (lgcn_bpr_fused_neg / lgcn_sorted_scatter_add_bpr) instead of a [B, d] table
-        self.nsc = (torch.empty((max(1, B), 4), dtype=torch.float32, device=dev)
-                    if self.small and self.neg_rowptr is not None else None)
         self.cf = torch.empty((3 * B, d), dtype=torch.float32, device=dev)
         # reg-gradient rows: materialised only for the large-batch sort path; the segment-plan path
         # forms their sums from the layer-0 rows (lgcn_reg_rows_add, the scatters' reg source)
@@ -273,34 +269,12 @@ def loss_fused(st, I: int, cols=None) -> bool:
     return cols is None and st.neg_rowptr is None and I > 0 and 1 <= st.B < _ffi.LOSS_FUSED_MAX_B
 
 
-def use_neg_scalars(st, cols=None) -> bool:
-    """The step's BPR writes the negatives' scalars instead of their dF rows (the sorted path;
-    not column-sharded; lgcn_amd.tuning neg_rows_recompute)."""
-    from . import tuning
-
-    return st.nsc is not None and cols is None and tuning.get().neg_rows_recompute
-
-
-def bpr_call(lib, st, out, uw, iw, U: int, N: int, B: int, d: int, div: float, mul: float, coeff: float, stream,
-             nsc: bool) -> None:
-    """lgcn_bpr_fused, or lgcn_bpr_fused_neg when the scatter recomputes the negatives' rows."""
-    args = (out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U, st.users.data_ptr(), st.pos.data_ptr(),
-            st.neg.data_ptr(), B, d, st.plan.touched.data_ptr(), div, mul, coeff, st.cf.data_ptr(), _ffi.ptr(st.cw),
-            st.terms.data_ptr())
-    if nsc:
-        _ffi.check(lib.lgcn_bpr_fused_neg(*args, st.nsc.data_ptr(), stream), "lgcn_bpr_fused_neg")
-    else:
-        _ffi.check(lib.lgcn_bpr_fused(*args, stream), "lgcn_bpr_fused")
-
-
 def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: float, store_unless, stream,
-                      uw, iw, coeff: float, loss=None, rows_from=None) -> None:
+                      uw, iw, coeff: float, loss=None) -> None:
     """dF rows of the step's negatives into the gradient tables and the first-occurrence flags
     (st.c2flag); the range scatter also parks each row's reg-rows sum (formed from the layer-0
     rows uw / iw) in its first-occurrence slot for add_negative_reg_rows after the backward.
-    loss = (terms, d, coeff, out): the step's loss sum in the same launch (loss_fused).
-    rows_from = F (the forward's [N, d] output): the BPR wrote the negatives' scalars (st.nsc), and
-    the sorted scatter recomputes their rows from F / W (lgcn_sorted_scatter_add_bpr)."""
+    loss = (terms, d, coeff, out): the step's loss sum in the same launch (loss_fused)."""
     B = st.B
     C = st.cf[2 * B:]
     reg = (None, uw.data_ptr(), iw.data_ptr(), U, coeff, B)
@@ -326,14 +300,6 @@ def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: 
                    "lgcn_group_keys(negatives)")
     # sorted path: no parked reg sums (add_negative_reg_rows forms them per row after the backward);
     # the first-occurrence flags are still written
-    if rows_from is not None:
-        _ffi.check(lib.lgcn_sorted_scatter_add_bpr(st.neg_rowptr.data_ptr(), st.neg_perm.data_ptr(), I, U, d,
-                                                   gu.data_ptr(), gi.data_ptr(), U, mul, div, st.c2flag.data_ptr(),
-                                                   _ffi.ptr(store_unless), rows_from.data_ptr(), None,
-                                                   rows_from.shape[0], uw.data_ptr(), iw.data_ptr(), U,
-                                                   st.users.data_ptr(), st.nsc.data_ptr(), st.plan.touched.data_ptr(),
-                                                   div, mul, stream), "lgcn_sorted_scatter_add_bpr")
-        return
     _ffi.check(lib.lgcn_sorted_scatter_add(st.neg_rowptr.data_ptr(), st.neg_perm.data_ptr(), I, U, C.data_ptr(), d,
                                            gu.data_ptr(), gi.data_ptr(), U, mul, div, None, None, None, 0, 0.0, 0,
                                            st.c2buf.data_ptr(), st.c2flag.data_ptr(), _ffi.ptr(store_unless), stream),
@@ -488,8 +454,11 @@ class FusedTrainStep:
             out = propagate_forward(uw.detach(), iw.detach(), st.plan, K)
             if not st.small:  # only the all-keys sort reads the negatives' global row keys
                 torch.add(st.neg, U, out=st.keys[2 * B:])
-            nsc = use_neg_scalars(st)
-            bpr_call(lib, st, out, uw, iw, U, N, B, d, div, mul, self.coeff, stream, nsc)
+            _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
+                                          st.users.data_ptr(), st.pos.data_ptr(), st.neg.data_ptr(), B, d,
+                                          st.plan.touched.data_ptr(), div, mul,
+                                          self.coeff, st.cf.data_ptr(), _ffi.ptr(st.cw), st.terms.data_ptr(),
+                                          stream), "lgcn_bpr_fused")
             fused = st.small and loss_fused(st, I)
             if not fused:
                 _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(),
@@ -506,7 +475,7 @@ class FusedTrainStep:
                      stream=stream)
                 # negatives: dF rows into g now, their reg rows parked (per row, first-occurrence slot)
                 scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, None, stream, uw, iw, self.coeff,
-                                  (st.terms, d, self.coeff, st.loss) if fused else None, rows_from=out if nsc else None)
+                                  (st.terms, d, self.coeff, st.loss) if fused else None)
                 propagate_backward_seeded(gu, gi, st.plan, K)
                 add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, self.coeff, stream)
                 add_negative_reg_rows(lib, st, gu, gi, U, d, uw, iw, self.coeff, stream)
@@ -532,7 +501,11 @@ class FusedTrainStep:
         column groups, then the gradient rows of its columns from the full sums."""
         c = self.cols
         if c is None:
-            bpr_call(lib, st, out, uw, iw, U, N, B, d, div, mul, self.coeff, stream, use_neg_scalars(st))
+            _ffi.check(lib.lgcn_bpr_fused(out.data_ptr(), None, N, uw.data_ptr(), iw.data_ptr(), U, U,
+                                          st.users.data_ptr(), st.pos.data_ptr(), st.neg.data_ptr(), B, d,
+                                          st.plan.touched.data_ptr(), div, mul,
+                                          self.coeff, st.cf.data_ptr(), _ffi.ptr(st.cw), st.terms.data_ptr(),
+                                          stream), "lgcn_bpr_fused")
             if not loss_fused(st, N - U):  # else the range scatter's launch sums it (_step_lazy)
                 _ffi.check(lib.lgcn_bpr_loss(st.terms.data_ptr(), B, d, self.coeff, st.loss.data_ptr(),
                                              st.loss_part.data_ptr(), stream), "lgcn_bpr_loss")
@@ -589,8 +562,7 @@ class FusedTrainStep:
                  stream=stream)
             # ... the negatives' rows added (stored where the row is outside the touched set)
             scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream, uw, iw, reg_coeff,
-                              (st.terms, d, self.coeff, st.loss) if loss_fused(st, I, self.cols) else None,
-                              rows_from=out if use_neg_scalars(st, self.cols) else None)
+                              (st.terms, d, self.coeff, st.loss) if loss_fused(st, I, self.cols) else None)
             propagate_backward_seeded(gu, gi, st.plan, K)
             add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, reg_coeff, stream)
             add_negative_reg_rows(lib, st, gu, gi, U, d, uw, iw, reg_coeff, stream)

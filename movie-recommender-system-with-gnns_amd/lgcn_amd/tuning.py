@@ -39,9 +39,6 @@ class Tuning:
     neg_grouping: str = "count"
     # batch size from which the negatives take the sorted scatter instead of the range scatter
     sorted_scatter_min_b: int = 49152
-    # sorted path: the BPR writes 4 scalars per negative and the scatter recomputes its dF row
-    # (lgcn_bpr_fused_neg / lgcn_sorted_scatter_add_bpr; bitwise) instead of a [B, d] table
-    neg_rows_recompute: bool = True
     # hub chunk (edges per lane-group chain) of a Cluster-GCN batch's propagation plan: None =
     # lgcn_amd.train_step.batch_chunk_for's measured rule (by the batch's edge count); > 0 = forced
     batch_chunk: int | None = None

@@ -468,17 +468,13 @@ def test_recall_parity_c1_size(gpu, tune):
         assert abs(hip_index[k] - ref_cpu[k]) <= 0.002, (k, stats)  # BASELINE.json north star
 
 
-@pytest.mark.parametrize("lazy,grouping,recompute", [(False, "count", True), (True, "count", True),
-                                                     (True, "radix", True), (True, "count", False)])
-def test_sorted_negatives_path_bitwise_range_path(gpu, tune, lazy, grouping, recompute):
+@pytest.mark.parametrize("lazy,grouping", [(False, "count"), (True, "count"), (True, "radix")])
+def test_sorted_negatives_path_bitwise_range_path(gpu, tune, lazy, grouping):
     """The large-B negatives path (the keys grouped by row — lgcn_group_keys, or one radix sort
     with tuning neg_grouping="radix" — then lgcn_sorted_scatter_add, taken from
     sorted_scatter_min_b triplets) gives bitwise the range-scatter path's losses and
-    parameters over 12 hipGraph-replayed steps (dense FusedAdam and row-lazy Adam). recompute
-    (tuning neg_rows_recompute, the default): the BPR writes 4 scalars per negative and the sorted
-    scatter recomputes its dF row from the F / W rows (lgcn_bpr_fused_neg,
-    lgcn_sorted_scatter_add_bpr) — still bitwise the range path, which reads the materialised rows."""
-    tune(neg_grouping=grouping, neg_rows_recompute=recompute)
+    parameters over 12 hipGraph-replayed steps (dense FusedAdam and row-lazy Adam)."""
+    tune(neg_grouping=grouping)
     from lgcn_amd import cluster as C
     from lgcn_amd.optim import FusedAdam, RowLazyAdam
     from lgcn_amd.train_step import FusedTrainStep
@@ -507,7 +503,6 @@ def test_sorted_negatives_path_bitwise_range_path(gpu, tune, lazy, grouping, rec
         step.sync()
         st = step.state(batches[-1].edge_index)
         assert (st.neg_rowptr is not None) == (min_b == 1)
-        assert (st.nsc is not None) == (min_b == 1)
         res.append((losses, m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
