@@ -431,6 +431,10 @@ int lgcn_bpr_fused_cols(const float* f_lo, const float* f_hi, int64_t f_split, c
 #define LGCN_LOSS_FUSED_MAX_B 16384
 int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* loss, float* partial,
                   lgcn_stream_t stream);
+/* acc[0] += (double)loss[0] * w (ABI 9): the harness's epoch loss, sum of batch loss * edges
+ * (reference utils/train_test.py:101-103 accumulates loss.item() * edges in Python floats: the same
+ * two double roundings), a node of each batch's captured step instead of three eager launches. */
+int lgcn_loss_accumulate(const float* loss, double w, double* acc, lgcn_stream_t stream);
 int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C, int64_t N, int32_t d,
                       float* out_lo, float* out_hi, int64_t split, int32_t add, float mul, float div,
                       lgcn_stream_t stream);

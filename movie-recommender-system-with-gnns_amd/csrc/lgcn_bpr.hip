@@ -645,6 +645,16 @@ __global__ __launch_bounds__(kBlock) void k_sorted_scatter(const int64_t* __rest
     }
 }
 
+// acc[0] += double(loss[0]) * w: the harness's epoch-loss sum (reference utils/train_test.py:101-103,
+// total_loss += loss.item() * edges, in Python floats) with the same two double roundings (product,
+// then sum; built without contraction), as one node of the batch's captured step.
+__global__ void k_loss_accumulate(const float* __restrict__ loss, double w, double* __restrict__ acc) {
+    if (threadIdx.x == 0) {
+        const double c = static_cast<double>(loss[0]) * w;
+        acc[0] = acc[0] + c;
+    }
+}
+
 // Second pass for the parked sums: each flagged slot b adds c2buf[b] to row keys[b] + key_offset.
 // Every row owns at most one flagged slot (its first occurrence) unless the scatter overflowed.
 template <int LPR, int NV>
@@ -984,6 +994,12 @@ int lgcn_bpr_loss(const float* terms, int64_t B, int32_t d, float coeff, float* 
     }
     k_bpr_loss<<<1, kLossBlock, 0, s>>>(terms, B, B, B, d, coeff, loss);
     return check_launch("k_bpr_loss");
+}
+
+int lgcn_loss_accumulate(const float* loss, double w, double* acc, lgcn_stream_t stream) {
+    if (!loss || !acc) return fail(LGCN_E_ARG, "lgcn_loss_accumulate: null pointer");
+    k_loss_accumulate<<<1, 64, 0, as_stream(stream)>>>(loss, w, acc);
+    return check_launch("k_loss_accumulate");
 }
 
 int lgcn_segment_rows(const int64_t* rowptr, const int32_t* perm, const float* C, int64_t N, int32_t d,

@@ -86,6 +86,7 @@ _SIGS = {
     "lgcn_bpr_fused_cols": ([_vp, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _f32, _f32,
                              _f32, _vp, _i32, _vp, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_bpr_loss": ([_vp, _i64, _i32, _f32, _vp, _vp, _vp], ctypes.c_int),
+    "lgcn_loss_accumulate": ([_vp, ctypes.c_double, _vp, _vp], ctypes.c_int),
     "lgcn_segment_rows": ([_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _i32, _f32, _f32, _vp], ctypes.c_int),
     "lgcn_range_scatter_add": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _i64,
                                 _f32, _i64, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),

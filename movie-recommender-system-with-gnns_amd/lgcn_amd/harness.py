@@ -92,13 +92,14 @@ class _Fast:
         uw, iw = model.user_embedding.weight, model.item_embedding.weight
         self.opt = RowLazyAdam(uw.data, iw.data, lr=self.lr, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=1.0,
                                max_steps=_MIN_STEPS)
-        from utils import helpers
-
         num_items, dev = model.num_items, uw.device
+        # the epoch's sum of loss * edges (reference utils/train_test.py:101-103), added on the
+        # device by each captured step (lgcn_loss_accumulate): no per-step torch ops
+        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
         # the negatives come from the harness's own sampler (reference utils/helpers.py:64-82):
         # the reference loop's draws, and whatever a caller substitutes for them
         self.step = FusedTrainStep(model, self.opt, lazy=True, graphs=True, max_entries=_MIN_STATES,
-                                   neg_sampler=lambda pos: helpers.sample_negative(pos, num_items, dev))
+                                   neg_sampler=_Sampler(num_items, dev), loss_acc=self.loss_acc)
         # device copies of host batches by content, so a batch keeps its plans and captured graph
         # from epoch to epoch even when the loader collates a new tensor each time
         self.dev_batches = ContentLRU(_MIN_STATES)
@@ -175,6 +176,28 @@ class _Fast:
             st["step"] = torch.tensor(float(self.opt.steps), dtype=torch.float32)
 
 
+class _Sampler:
+    """utils.helpers.sample_negative(pos, num_items, device) as the step's negatives sampler. While
+    that function is the reference's own (not patched by a caller), draw_into writes the same
+    torch.randint(0, I, (B,)) draw straight into the batch's buffer (out=: the same kernel on the same
+    shape, so the same values and generator offsets) instead of drawing a new tensor and copying it."""
+
+    def __init__(self, num_items: int, device):
+        from utils import helpers
+
+        self.helpers = helpers
+        self.num_items, self.device = int(num_items), device
+
+    def __call__(self, pos):
+        return self.helpers.sample_negative(pos, self.num_items, self.device)
+
+    def draw_into(self, out, pos) -> None:
+        if self.helpers.sample_negative is self.helpers.REFERENCE_SAMPLE_NEGATIVE:
+            torch.randint(0, self.num_items, (pos.shape[0],), device=self.device, out=out)
+        else:
+            out.copy_(self(pos))
+
+
 _FAST: "weakref.WeakKeyDictionary[torch.optim.Optimizer, _Fast]" = weakref.WeakKeyDictionary()
 
 
@@ -208,6 +231,7 @@ def train_epoch(model, optimizer, batches, device):
         n = None
     fast.load_state(optimizer)
     fast.size_for(n)
+    fast.loss_acc.zero_()
     total, total_w, steps, leftover = None, 0, 0, None
     U = model.num_users
     from ._cache import prefetch
@@ -231,14 +255,12 @@ def train_epoch(model, optimizer, batches, device):
             if fast.opt.steps + 1 > fast.opt.max_steps:  # a loader without len(): grow mid-epoch
                 fast.step.sync()  # every row current before the constants are regenerated
                 fast.reserve(fast.opt.steps + 1)
-            loss = fast.step.step(_Batch(ei))
+            fast.step.step(_Batch(ei))  # adds double(loss) * edges to fast.loss_acc on the device
             steps += 1
-            w = int(ei.shape[1])
-            total_w += w
-            contrib = loss.detach().double() * w
-            total = contrib if total is None else total + contrib
+            total_w += int(ei.shape[1])
     finally:
         if steps:
+            total = fast.loss_acc.clone()
             fast.store_state(optimizer)
     return total, total_w, leftover, steps
 

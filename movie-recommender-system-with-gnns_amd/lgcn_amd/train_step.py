@@ -176,6 +176,7 @@ class _BatchState:
         if self.users.numel() != self.pos.numel():
             raise ValueError("batch is not a symmetric bipartite edge list: users and positives differ in count")
         B = self.B = int(self.users.numel())
+        self.n_edges = int(edge_index.shape[1])  # the harness's loss weight (reference :101)
         self.neg = torch.empty(B, dtype=torch.int64, device=dev)
         self.keys = torch.empty(3 * B, dtype=torch.int64, device=dev)
         self.keys[:B] = self.users
@@ -334,7 +335,7 @@ class FusedTrainStep:
 
     def __init__(self, model, optimizer, bpr_coeff: float = 5e-3, world: int = 1, max_entries: int = 1024,
                  graphs: bool = False, lazy: bool = False, exchange=None, neg_seed: int | None = None,
-                 cols: ColumnGroup | None = None, neg_sampler=None):
+                 cols: ColumnGroup | None = None, neg_sampler=None, loss_acc: torch.Tensor | None = None):
         """graphs=True: the first step of each batch runs eagerly, then the whole step (gradients
         and, at world == 1, the optimizer — which must be a capturable FusedAdam) is captured in a
         per-batch hipGraph and replayed from then on; negatives still come from the global CUDA
@@ -352,7 +353,9 @@ class FusedTrainStep:
         each batch's step is captured as graphs cut at the two collectives (_SegmentedGraph).
         neg_sampler (pos_items [B] -> item ids [B]): draw the negatives with it (the harness passes
         utils.helpers.sample_negative, so what that function draws — patched or not — is what the
-        step trains on); default: torch.randint(0, I, (B,)) into the batch's buffer, the same draws."""
+        step trains on); default: torch.randint(0, I, (B,)) into the batch's buffer, the same draws.
+        loss_acc (lazy; device float64 [1]): each step adds double(loss) * its batch's edge count to
+        it (lgcn_loss_accumulate, inside the captured step) — the harness's epoch-loss sum."""
         self.model = model
         self.optimizer = optimizer
         self.coeff = float(bpr_coeff)
@@ -389,6 +392,9 @@ class FusedTrainStep:
             raise ValueError("an OwnerExchange needs lazy=True (RowLazyAdam)")
         self.neg_seed = neg_seed
         self.neg_sampler = neg_sampler
+        if loss_acc is not None and (loss_acc.dtype != torch.float64 or loss_acc.numel() < 1 or not lazy):
+            raise ValueError("loss_acc must be a device float64 tensor of >= 1 element (lazy=True)")
+        self.loss_acc = loss_acc
         self._gen = None
         self._k = 0  # steps taken (the index of the next step)
         self._owner_graphs = None
@@ -423,7 +429,10 @@ class FusedTrainStep:
         dev = m.user_embedding.weight.device
         k = self._k if k is None else k
         if self.neg_sampler is not None:
-            st.neg.copy_(self.neg_sampler(st.pos))
+            if hasattr(self.neg_sampler, "draw_into"):
+                self.neg_sampler.draw_into(st.neg, st.pos)
+            else:
+                st.neg.copy_(self.neg_sampler(st.pos))
             st.neg_step = k
             return
         gen = None
@@ -587,6 +596,9 @@ class FusedTrainStep:
                                               st.touched_rows.numel(), st.neg.data_ptr(), B, U,
                                               st.c2flag.data_ptr(), st.plan.touched.data_ptr(), ex.cap,
                                               ex.ids.data_ptr(), ex.rows.data_ptr(), stream), "lgcn_rows_pack")
+            if self.loss_acc is not None:
+                _ffi.check(lib.lgcn_loss_accumulate(st.loss.data_ptr(), float(st.n_edges), self.loss_acc.data_ptr(),
+                                                    stream), "lgcn_loss_accumulate")
         return st.loss
 
     def _lazy_update(self, st: _BatchState) -> None:

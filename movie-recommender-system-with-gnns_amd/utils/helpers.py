@@ -25,6 +25,11 @@ def sample_negative(pos_idx: torch.Tensor, num_items: int, device) -> torch.Tens
     return torch.randint(0, num_items, (pos_idx.shape[0],), device=device)
 
 
+# the function above as defined here, whatever a caller later patches sample_negative to
+# (lgcn_amd.harness draws in place only while the two are the same object)
+REFERENCE_SAMPLE_NEGATIVE = sample_negative
+
+
 def get_triplets_indices(edge_index: torch.Tensor, num_users: int, num_items: int,
                          device) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """(user ids, positive item ids, negative item ids) of a batch (reference utils/helpers.py:84-102)."""
