@@ -611,10 +611,15 @@ class ReducePlan:
                          mul, n_split_big=getattr(direction, "n_split_big", -1))
 
     def _run(self, p, dev) -> None:
+        import contextlib
         import ctypes
 
-        _ffi.check(_ffi.load().lgcn_spmm_pass(ctypes.byref(p), self.shards.N, self.d, 3, _ffi.stream_of(dev)),
-                   "lgcn_spmm_pass")
+        from . import propagate
+
+        timer = propagate._launch_timer  # bench.py's launch brackets (one pass: items + combine)
+        with (timer(self.d, 1) if timer is not None else contextlib.nullcontext()):
+            _ffi.check(_ffi.load().lgcn_spmm_pass(ctypes.byref(p), self.shards.N, self.d, 3, _ffi.stream_of(dev)),
+                       "lgcn_spmm_pass")
 
     def run_partial(self, x_users: torch.Tensor, part_items: torch.Tensor) -> None:
         U = self.shards.U
@@ -635,8 +640,14 @@ class ReducePlan:
         pa = self._pass(self.partial, (x_users, part_items, U), None, None, (part_items, part_items, U),
                         _ffi.EPI_STORE, 1.0, 1.0)
         pb = self._pass(self.users, (x_items, x_items, U), e, y, acc, mode, div, mul)
-        _ffi.check(_ffi.load().lgcn_spmm_pair(ctypes.byref(pa), ctypes.byref(pb), self.shards.N, self.d, 3,
-                                              _ffi.stream_of(x_users.device)), "lgcn_spmm_pair")
+        import contextlib
+
+        from . import propagate
+
+        timer = propagate._launch_timer  # one bracket over both passes: counted as their two launches
+        with (timer(self.d, 2) if timer is not None else contextlib.nullcontext()):
+            _ffi.check(_ffi.load().lgcn_spmm_pair(ctypes.byref(pa), ctypes.byref(pb), self.shards.N, self.d, 3,
+                                                  _ffi.stream_of(x_users.device)), "lgcn_spmm_pair")
 
     def finish_items(self, x0i: torch.Tensor, layers: list, last_share: torch.Tensor, out_i: torch.Tensor,
                      div: float, mul: float) -> None:
