@@ -252,3 +252,20 @@ def test_compute_recall_at_k_cpu_ties_equals_reference_on_cpu(gpu, tune):
         assert got_cpu == ref_cpu, (k, got_cpu, ref_cpu)
         assert got_index == pytest.approx(ref_index, rel=1e-6, abs=0), (k, got_index, ref_index)
         assert got_index != got_cpu
+
+
+def test_cpu_ties_query_blocks(gpu, tune, monkeypatch):
+    """recall_ties="cpu" writes dense score rows per query block (lgcn_amd.recall.STL_BLOCK_BYTES):
+    several blocks (the padded queries of the last one included) give the one-block hits."""
+    from lgcn_amd import recall as RC
+
+    rng = np.random.default_rng(31)
+    users, pos, neg = _dup_rows(rng, 400, 32, 2000, 2000, 700)
+    t = lambda a: torch.from_numpy(a).to(gpu)
+    picked = torch.from_numpy(rng.choice(700, 600, replace=False))
+    for k in (20, 100):  # partial_sort (k * 64 <= 4000) and nth_element
+        one = RC.topk_hits(t(users), picked, t(pos), t(neg), k, ties="cpu").cpu()
+        monkeypatch.setattr(RC, "STL_BLOCK_BYTES", 8 * 4000 * 128)  # 128 queries per block
+        many = RC.topk_hits(t(users), picked, t(pos), t(neg), k, ties="cpu").cpu()
+        monkeypatch.setattr(RC, "STL_BLOCK_BYTES", 1 << 30)
+        assert torch.equal(one, many), k

@@ -21,8 +21,11 @@ def main():
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--layers", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--ties", default="index", help="lgcn_amd.tuning recall_ties: index | cpu")
     args = ap.parse_args()
-    from lgcn_amd import synth
+    from lgcn_amd import synth, tuning
+
+    tuning.set_tuning(recall_ties=args.ties)
     from models.light_gcn import LightGCN
     from utils import train_test as T
 
@@ -58,7 +61,7 @@ def main():
             np.random.seed(r)
             rec, t_rec = timed(lambda: T.compute_recall_at_k((embs[1], embs[3], embs[5]), k=100))
         _, t_eval = timed(lambda: T.evaluate(model, D(), dev, top_k=100))
-        print(f"E_val={ei.shape[1]} B={embs[0].shape[0]} d={args.dim}: embeddings {t_emb:.2f} ms, "
+        print(f"ties={args.ties} E_val={ei.shape[1]} B={embs[0].shape[0]} d={args.dim}: embeddings {t_emb:.2f} ms, "
               f"loss {t_loss:.2f} ms, recall@100 {t_rec:.2f} ms (={rec:.3e}), evaluate {t_eval:.2f} ms", flush=True)
 
 
