@@ -785,57 +785,6 @@ class ItemReducer:
             torch.cuda.current_stream(device).wait_event(handle)
 
 
-_REDUCE_STREAMS: dict = {}
-
-
-def _forward_reduced_streams(x0u, x0i, rplan, K, reducer, part, share, yu, e, acc, out_u, out_i, mode_of, start,
-                             div, mul):
-    """The overlapped order with each layer's two passes on two streams (tuning reduce_streams):
-    the partial passes (and the reductions they start) on a high-priority stream, the user passes
-    on another, so a layer's user pass fills the GPU beside its partial pass instead of after it —
-    the pair launch's overlap — while each reduction still starts as soon as its partial pass
-    ends. Dependencies as the one-stream order's: P_k after U_{k-1} (it reads those rows); U_k after
-    layer k-1's reduction and after P_{k-1} (it overwrites the rows P_{k-1} read). The same kernels
-    on the same data: bitwise the one-stream result."""
-    dev = x0u.device
-    ss = _REDUCE_STREAMS.get(dev)
-    if ss is None:
-        ss = _REDUCE_STREAMS[dev] = (torch.cuda.Stream(dev, priority=-1), torch.cuda.Stream(dev))
-    sp, su = ss
-    main = torch.cuda.current_stream(dev)
-    sp.wait_stream(main)
-    su.wait_stream(main)
-    pending, u_done, p_done = None, None, None
-    for k in range(1, K + 1):
-        src_u = x0u if k == 1 else yu[(k - 2) % 2]
-        src_i = x0i if k == 1 else part[k - 2]
-        mode = mode_of(k)
-        final = mode in (_ffi.EPI_FINAL_E, _ffi.EPI_FINAL_ACC)
-        y = yu[(k - 1) % 2] if k < K else None
-        ue = e if mode in (_ffi.EPI_INIT, _ffi.EPI_FINAL_E) else None
-        udiv, umul = (div, mul) if final else (1.0, 1.0)
-        with torch.cuda.stream(sp):
-            if u_done is not None:
-                sp.wait_event(u_done)
-            rplan.run_partial(src_u, part[k - 1])
-            started = start(k)
-            p_prev, p_done = p_done, torch.cuda.Event()
-            p_done.record(sp)
-        with torch.cuda.stream(su):
-            if p_prev is not None:  # P_{k-1} done (and a host-memory reduction's copy back)
-                su.wait_event(p_prev)
-            reducer.wait(pending, dev)
-            rplan.run_users(src_i, ue, acc, y, mode, udiv, umul)
-            u_done = torch.cuda.Event()
-            u_done.record(su)
-        pending = started
-    main.wait_stream(sp)
-    main.wait_stream(su)
-    reducer.wait(pending, dev)
-    rplan.finish_items(x0i, part[:K - 1], share, out_i, div, mul)
-    return out_u, out_i
-
-
 def propagate_forward_reduced(x0u: torch.Tensor, x0i: torch.Tensor, rplan, K: int,
                               reducer: ItemReducer, fused: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
     """(users [U, d], items [I, d]): the LightGCN final embedding of this row group's users and of
@@ -881,11 +830,6 @@ def propagate_forward_reduced(x0u: torch.Tensor, x0i: torch.Tensor, rplan, K: in
             return reducer.start(part[k - 1])
         return reducer.start_scatter(part[k - 1], share, rplan.g)  # the last layer: this member's share
 
-    from . import tuning
-
-    if not fused and tuning.get().reduce_streams and x0u.is_cuda:
-        return _forward_reduced_streams(x0u, x0i, rplan, K, reducer, part, share, yu, e, acc, out_u, out_i,
-                                        mode_of, start, div, mul)
     pending = None  # the reduction in flight
     for k in range(1, K + 1):
         src_u = x0u if k == 1 else yu[(k - 2) % 2]

@@ -53,9 +53,6 @@ class Tuning:
     harness_fused: bool = True
     # run the exchanges' RCCL branches even on a gloo group (tests: gloo carries the bytes)
     device_collectives: bool = False
-    # reduce-mode C2 grid, overlapped order: a layer's partial and user passes on two streams
-    # (lgcn_amd.sharded._forward_reduced_streams) instead of one after the other
-    reduce_streams: bool = False
     # --- native (lgcn_tuning_t) -----------------------------------------------------------------
     spmm_tail: int = -1
     spmm_index_rounds: int = 0

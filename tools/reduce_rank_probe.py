@@ -76,9 +76,6 @@ def main():
                 graph = order.endswith("+g")
                 base = order[:-2] if graph else order
                 fused = base.startswith("fused")
-                from lgcn_amd import tuning as _tn
-
-                _tn.set_tuning(reduce_streams=base.startswith("overlapped-s"))
                 unpacked = base.endswith("-u")
                 nb = {}
                 for dr in (rplan.users, rplan.partial):
