@@ -100,6 +100,8 @@ def _device_digest_start(t: torch.Tensor) -> _PendingDigest:
     stream.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(stream):
         c = t.detach().contiguous()
+        if c.data_ptr() % 8:  # a view at an odd byte offset: digest an aligned copy of the same bytes
+            c = c.clone()
         nbytes = c.numel() * c.element_size()
         _ffi.check(lib.lgcn_digest128(c.data_ptr() if nbytes else None, nbytes, ring.ws.data_ptr(), ring.ws.numel(),
                                       ring.out[s].data_ptr(), _ffi.stream_of(dev)), "lgcn_digest128")

@@ -88,6 +88,10 @@ def test_digest_sensitivity(gpu):
         seen.add(d)
     # a non-contiguous view digests its contiguous content
     assert _dev_digest(ei.to(gpu).t().contiguous().t()) == base
+    # a byte view at an odd offset: the same bytes' digest (an aligned copy is hashed)
+    raw = torch.arange(0, 37, dtype=torch.uint8)
+    dev_raw = raw.to(gpu)
+    assert _dev_digest(dev_raw[3:]) == digest_ref(raw[3:].numpy().tobytes())
 
 
 class _B:
