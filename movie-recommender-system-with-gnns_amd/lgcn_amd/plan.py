@@ -322,8 +322,11 @@ class PropagationPlan:
 class PlanCache:
     """Plans keyed by the edge_index's content (lgcn_amd._cache: the tensor object itself while it
     lives unmodified, else a digest of its bytes) plus (num_nodes, side_split): a tensor modified in
-    place never hits a stale plan, and a loader that collates a new tensor of the same edges each
-    epoch reuses its plan. Least recently used plans are evicted beyond max_entries."""
+    place through torch (which bumps its version counter) is rehashed, and a loader that collates a
+    new tensor of the same edges each epoch reuses its plan. Writes torch's counter does not see
+    (through numpy, .data, DLPack or a raw pointer) leave the old key: hand over a new tensor object
+    then, or call lgcn_amd._cache.forget(t). Least recently used plans are evicted beyond
+    max_entries."""
 
     def __init__(self, max_entries: int = 1024, chunk: int = DEFAULT_CHUNK):
         from ._cache import ContentLRU
