@@ -30,7 +30,9 @@ s = s.replace(epi, """#ifdef LGCN_VARIANT_NO_EPI
 """ + epi, 1)
 open(p, "w").write(s)
 EOF
-F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared -ffp-contract=off -I$R/include"
+# the tree's provenance hash (as tools/build_variant.py links it), so lgcn_amd._ffi loads the variant
+SHA=$(cd "$R" && python3 -c "import __graft_entry__ as g; print(g._ffi_module().source_sha256())")
+F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared -ffp-contract=off -I$R/include -DLGCN_SOURCE_SHA256=$SHA"
 SRC=$(ls "$T"/src/*.hip "$T"/src/*.cpp)
 for v in "$@"; do
   /opt/rocm/bin/hipcc $F -DLGCN_VARIANT_$v $SRC -o "$T/$v.so" &
