@@ -38,7 +38,7 @@ extern "C" {
 
 typedef void* lgcn_stream_t; /* a hipStream_t; NULL = the null stream */
 
-#define LGCN_ABI_VERSION 9
+#define LGCN_ABI_VERSION 10
 
 #define LGCN_OK 0
 #define LGCN_E_ARG (-1)         /* bad size / null pointer / unsupported argument */
@@ -503,6 +503,37 @@ int lgcn_flagged_rows_add(const int64_t* keys, int64_t B, int64_t key_offset, co
                           const uint8_t* c2flag, int32_t d, float* out_lo, float* out_hi, int64_t split,
                           lgcn_stream_t stream);
 
+/* The reg-gradient rows of a batch step by their occurrence counts (ABI 10): row r's gradient gets
+ * nf copies of kreg * W[r] (its (user, positive) occurrences, fixed_rowptr[r+1] - fixed_rowptr[r])
+ * and then nn copies (its negatives': neg_rowptr[r-neg_off+1] - neg_rowptr[r-neg_off], or
+ * neg_count[r - neg_off], for neg_off <= r < neg_off + neg_rows), each sum formed in sequence from 0
+ * and added only when it has copies, kreg = coeff * 2 / (B * d) — exactly what lgcn_reg_rows_add
+ * then lgcn_flagged_rows_add / lgcn_grouped_reg_add add after the backward (reference
+ * utils/train_test.py:38-41). lgcn_row_grad_norm_reg and lgcn_row_adam_reg form them on the fly
+ * (the norm from W, the update from the parameter rows before any replay — the same rows), so the
+ * single-GPU step needs neither pass nor a parked sum. fixed_rowptr nullable (no fixed copies). */
+typedef struct {
+    const float* w_lo; /* the layer-0 tables (the parameters), split at w_split rows */
+    const float* w_hi;
+    int64_t w_split;
+    float coeff;
+    int64_t B; /* triplets in the batch (>= 1) */
+    const int64_t* fixed_rowptr; /* [N + 1] or NULL */
+    const int64_t* neg_rowptr;   /* [neg_rows + 1] (grouped negatives) — or ... */
+    const int32_t* neg_count;    /* ... [neg_rows] (lgcn_range_scatter_add_counts); exactly one when neg_rows > 0 */
+    int64_t neg_off;
+    int64_t neg_rows;
+} lgcn_reg_rows_t;
+/* lgcn_range_scatter_add for the reg rows' counted form (ABI 10): no second source, no parked sum;
+ * instead reg_count[r] (int32[nrows], every row written) = the number of keys of row r, and c2flag as
+ * always. terms (nullable): with loss / loss_B / loss_d / loss_coeff, the step's loss as
+ * lgcn_range_scatter_add_loss sums it. */
+int lgcn_range_scatter_add_counts(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
+                                  int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
+                                  uint8_t* c2flag, int32_t* overflow, const uint8_t* store_unless, int32_t* reg_count,
+                                  const float* terms, int64_t loss_B, int32_t loss_d, float loss_coeff, float* loss,
+                                  lgcn_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * Row-lazy Adam (lgcn_rowadam.hip) for the sparse batch step: exact replay of the zero-gradient
  * steps a row missed, when the row is next touched (reference utils/train_test.py:95-96; same
@@ -534,6 +565,17 @@ int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int3
                        int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
                        const uint8_t* skip_b, float max_norm, float* ws, float* out, int64_t* step_advance,
                        lgcn_stream_t stream);
+/* lgcn_row_adam (mode 1 or 3) and lgcn_row_grad_norm over g + the step's reg rows (lgcn_reg_rows_t,
+ * ABI 10): bitwise those calls after lgcn_reg_rows_add and the negatives' reg pass; g is not written. */
+int lgcn_row_adam_reg(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_lo, float* m_hi, float* v_lo,
+                      float* v_hi, int64_t split, int32_t d, const int32_t* rows_a, int64_t n_a, const int64_t* keys_b,
+                      int64_t n_b, int64_t off_b, const uint8_t* first_b, const uint8_t* skip_b, int32_t* last,
+                      int64_t* step, const float* consts, float one_minus_beta1, float beta2, float one_minus_beta2,
+                      float eps, const float* clip, int32_t mode, const lgcn_reg_rows_t* reg, lgcn_stream_t stream);
+int lgcn_row_grad_norm_reg(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
+                           int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
+                           const uint8_t* skip_b, float max_norm, float* ws, float* out, int64_t* step_advance,
+                           const lgcn_reg_rows_t* reg, lgcn_stream_t stream);
 /* The clip norm split for the owner-sharded exchange (each rank owns some rows; the norm is over
  * all ranks' rows): lgcn_row_grad_sqnorm writes the lgcn_row_grad_norm_workspace_floats() block
  * partials of the listed rows' sum of squares (fixed block assignment: deterministic for a

@@ -18,6 +18,7 @@
 #include <climits>
 
 #include "lgcn_common.h"
+#include "lgcn_reg.h"
 
 using namespace lgcn;
 
@@ -40,24 +41,13 @@ struct RegSrc {
     int64_t B;
 };
 
-__device__ __forceinline__ float reg_scale(float coeff, int64_t B, int32_t d) {
-    // the same float expression as k_bpr_fused's kreg
-    return coeff * 2.0f / (static_cast<float>(B) * static_cast<float>(d));
-}
-
-// acc = (((0 + v) + v) + ...) n times, v = kreg * W[row]: lane l's NV float4 slots
+// acc = (((0 + v) + v) + ...) n times, v = kreg * W[row] (lgcn_reg.h): lane l's NV float4 slots
 template <int LPR, int NV>
 __device__ __forceinline__ void reg_sum(const RegSrc& r, int64_t row, int32_t d, int64_t n, int l, float4 (&acc)[NV]) {
     const float kreg = reg_scale(r.coeff, r.B, d);
     const float4* w = reinterpret_cast<const float4*>(row < r.w_split ? r.w_lo + row * d : r.w_hi + (row - r.w_split) * d) + l;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        const float4 x = w[k * LPR];
-        const float4 v = make_float4(kreg * x.x, kreg * x.y, kreg * x.z, kreg * x.w);
-        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int64_t i = 0; i < n; ++i) s = make_float4(s.x + v.x, s.y + v.y, s.z + v.z, s.w + v.w);
-        acc[k] = s;
-    }
+    for (int k = 0; k < NV; ++k) acc[k] = reg_copies(w[k * LPR], kreg, n);
 }
 
 template <int LPR>
@@ -378,7 +368,8 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                                                             RegSrc reg,
                                                             float* __restrict__ c2buf, uint8_t* __restrict__ c2flag,
                                                             int* __restrict__ overflow,
-                                                            const uint8_t* __restrict__ store_unless, LossArgs la) {
+                                                            const uint8_t* __restrict__ store_unless,
+                                                            int32_t* __restrict__ reg_count, LossArgs la) {
     static_assert(kRSBlock == kLossBlock, "the loss workgroup needs the loss block's size (its association)");
     if (la.loss != nullptr && blockIdx.x == gridDim.x - 1) {
         bpr_loss_block(la.terms, la.B, la.B, la.B, la.d, la.coeff, la.loss);
@@ -386,6 +377,9 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
     }
     constexpr int GPB = kRSBlock / LPR;
     const bool second = C2 != nullptr || reg.w_lo != nullptr;  // a second (parked) sum per row
+    // reg_count (ABI 10): each row's occurrence count instead of a parked sum (the clip norm and
+    // the update form the reg rows from it); the flags are written either way
+    const bool flags = second || reg_count != nullptr;
     __shared__ int lkey[kRangeCap];
     __shared__ int lidx[kRangeCap];
     __shared__ int wave_cnt[kRSWaves];
@@ -403,6 +397,8 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
     const unsigned long long below = (1ull << lane) - 1ull;
+    if (reg_count)  // every row of the range: 0 unless it has keys (the barrier below orders the stores)
+        for (int64_t i = lo + threadIdx.x; i < hi; i += kRSBlock) reg_count[i] = 0;
     if (threadIdx.x == 0) list_n = 0;
     __syncthreads();
     int64_t base = 0;
@@ -430,7 +426,7 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
             for (int j = 0; j < kRSChunks; ++j) {
                 const int64_t bj = base + (int64_t(wv) * kRSChunks + j) * 64 + lane;
                 // keys no workgroup owns (outside [0, nrows)): workgroup 0 clears their flag
-                if (second && blockIdx.x == 0 && bj < B && (kv[j] < 0 || kv[j] >= nrows)) c2flag[bj] = 0;
+                if (flags && blockIdx.x == 0 && bj < B && (kv[j] < 0 || kv[j] >= nrows)) c2flag[bj] = 0;
             }
 #pragma unroll
             for (int j = 0; j < kRSChunks; ++j) {
@@ -495,7 +491,7 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                     }
             }
             // every b is in exactly one list: its flag is written here (1 = the row's parked C2 sum)
-            if (second && l == 0) c2flag[lidx[e]] = first ? 1 : 0;
+            if (flags && l == 0) c2flag[lidx[e]] = first ? 1 : 0;
             if (!first) continue;
             float4 acc[NV], acc2[NV];
 #pragma unroll
@@ -525,6 +521,7 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                 }
             }
             const int64_t row = lo + key + key_offset;
+            if (reg_count && l == 0) reg_count[lo + key] = static_cast<int32_t>(occ);
             if (second) {  // second source: park the row's sum in the slot of its first occurrence
                 if (!C2) reg_sum<LPR, NV>(reg, row, d, occ, l, acc2);
                 float4* cb = reinterpret_cast<float4*>(c2buf + int64_t(lidx[e]) * d) + l;
@@ -679,7 +676,8 @@ __global__ __launch_bounds__(kBlock) void k_flagged_rows_add(const int64_t* __re
 template <int LPR, int NV>
 int launch_rs(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C, int32_t d, float* lo,
               float* hi, int64_t split, float mul, float div, const float* C2, RegSrc reg, float* c2buf,
-              uint8_t* c2flag, int* overflow, const uint8_t* store_unless, const LossArgs& la, hipStream_t s) {
+              uint8_t* c2flag, int* overflow, const uint8_t* store_unless, int32_t* reg_count, const LossArgs& la,
+              hipStream_t s) {
     // every workgroup streams all B keys once; enough workgroups that each keeps ~<= 256 entries
     // on average (the list holds kRangeCap), at least 256 (one per CU)
     int64_t wgs = B / 256 + 1;
@@ -691,7 +689,7 @@ int launch_rs(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset,
     k_range_scatter<LPR, NV><<<dim3(static_cast<unsigned>(grid)), kRSBlock, 0, s>>>(keys, B, nrows, span, key_offset, C, d,
                                                                                  lo, hi, split, mul, div, C2, reg,
                                                                                  c2buf, c2flag, overflow, store_unless,
-                                                                                 la);
+                                                                                 reg_count, la);
     return check_launch("k_range_scatter");
 }
 
@@ -794,22 +792,23 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 int range_scatter(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C, int32_t d,
                   float* out_lo, float* out_hi, int64_t split, float mul, float div, const float* C2,
                   const float* reg_w_lo, const float* reg_w_hi, int64_t reg_w_split, float reg_coeff, int64_t reg_B,
-                  float* c2buf, uint8_t* c2flag, int32_t* overflow, const uint8_t* store_unless, const LossArgs& la,
-                  lgcn_stream_t stream) {
+                  float* c2buf, uint8_t* c2flag, int32_t* overflow, const uint8_t* store_unless, int32_t* reg_count,
+                  const LossArgs& la, lgcn_stream_t stream) {
     const bool second = C2 != nullptr || reg_w_lo != nullptr;
     if (B < 0 || d <= 0 || nrows < 0 || (B > 0 && (!keys || !C || !out_lo)) || (second && (!c2buf || !c2flag)) ||
-        (C2 && reg_w_lo))
+        (C2 && reg_w_lo) || (reg_count && (second || !c2flag)))
         return fail(LGCN_E_ARG, "lgcn_range_scatter_add: bad args");
     if (B == 0) return LGCN_OK;
     if (nrows == 0)  // no key is in range: nothing to add, every flag 0
-        return second ? check_hip(hipMemsetAsync(c2flag, 0, static_cast<size_t>(B), as_stream(stream)), "memset c2flag")
-                      : LGCN_OK;
+        return (second || reg_count) ? check_hip(hipMemsetAsync(c2flag, 0, static_cast<size_t>(B), as_stream(stream)),
+                                                 "memset c2flag")
+                                     : LGCN_OK;
     if (d % 4 != 0 || !al16(C) || !al16(out_lo) || (out_hi && !al16(out_hi)) || (C2 && !al16(C2)) ||
         (second && !al16(c2buf)) || (reg_w_lo && (!al16(reg_w_lo) || (reg_w_hi && !al16(reg_w_hi)))))
         return fail(LGCN_E_UNSUPPORTED, "lgcn_range_scatter_add: needs d %% 4 == 0 and aligned rows");
     hipStream_t s = as_stream(stream);
     const RegSrc reg{reg_w_lo, reg_w_hi, reg_w_split, reg_coeff, reg_B};
-#define LGCN_RS(L, V) launch_rs<L, V>(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg, c2buf, c2flag, overflow, store_unless, la, s)
+#define LGCN_RS(L, V) launch_rs<L, V>(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg, c2buf, c2flag, overflow, store_unless, reg_count, la, s)
     switch (d) {
         case 8: return LGCN_RS(2, 1);
         case 16: return LGCN_RS(4, 1);
@@ -865,7 +864,7 @@ int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_
                            float reg_coeff, int64_t reg_B, float* c2buf, uint8_t* c2flag, int32_t* overflow,
                            const uint8_t* store_unless, lgcn_stream_t stream) {
     return range_scatter(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg_w_lo, reg_w_hi,
-                         reg_w_split, reg_coeff, reg_B, c2buf, c2flag, overflow, store_unless,
+                         reg_w_split, reg_coeff, reg_B, c2buf, c2flag, overflow, store_unless, nullptr,
                          LossArgs{nullptr, 0, 0, 0.f, nullptr}, stream);
 }
 
@@ -879,8 +878,23 @@ int lgcn_range_scatter_add_loss(const int64_t* keys, int64_t B, int64_t nrows, i
         return fail(LGCN_E_ARG, "lgcn_range_scatter_add_loss: bad loss args (B=%lld; the single-block sum needs "
                     "1 <= B < %d, and a scatter with work)", (long long)loss_B, LGCN_LOSS_FUSED_MAX_B);
     return range_scatter(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg_w_lo, reg_w_hi,
-                         reg_w_split, reg_coeff, reg_B, c2buf, c2flag, overflow, store_unless,
+                         reg_w_split, reg_coeff, reg_B, c2buf, c2flag, overflow, store_unless, nullptr,
                          LossArgs{terms, loss_B, loss_d, loss_coeff, loss}, stream);
+}
+
+int lgcn_range_scatter_add_counts(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
+                                  int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
+                                  uint8_t* c2flag, int32_t* overflow, const uint8_t* store_unless, int32_t* reg_count,
+                                  const float* terms, int64_t loss_B, int32_t loss_d, float loss_coeff, float* loss,
+                                  lgcn_stream_t stream) {
+    if (!c2flag || !reg_count) return fail(LGCN_E_ARG, "lgcn_range_scatter_add_counts: null c2flag / reg_count");
+    if (terms && (!loss || loss_B < 1 || loss_d <= 0 || loss_B >= LGCN_LOSS_FUSED_MAX_B || B <= 0 || nrows <= 0))
+        return fail(LGCN_E_ARG, "lgcn_range_scatter_add_counts: bad loss args (B=%lld; the single-block sum needs "
+                    "1 <= B < %d, and a scatter with work)", (long long)loss_B, LGCN_LOSS_FUSED_MAX_B);
+    return range_scatter(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, nullptr, nullptr, nullptr,
+                         0, 0.f, 0, nullptr, c2flag, overflow, store_unless, reg_count,
+                         terms ? LossArgs{terms, loss_B, loss_d, loss_coeff, loss} : LossArgs{nullptr, 0, 0, 0.f, nullptr},
+                         stream);
 }
 
 

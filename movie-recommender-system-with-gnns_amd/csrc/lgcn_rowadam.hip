@@ -22,6 +22,7 @@
 
 #include "lgcn_common.h"
 #include "lgcn_exact.h"
+#include "lgcn_reg.h"
 
 using namespace lgcn;
 
@@ -202,7 +203,7 @@ template <int LPR, int NV>
 __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int64_t n_rows, int32_t* __restrict__ last,
                                                      int32_t* __restrict__ claim, const int64_t* __restrict__ step,
                                                      const float4* __restrict__ consts, AdamK k,
-                                                     const float* __restrict__ clip, int mode) {
+                                                     const float* __restrict__ clip, int mode, RegRows R) {
     constexpr int GPB = kBlock / LPR;
     const int g = threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
@@ -239,6 +240,12 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
     if (!upd && from > upto) return;
     const float coef = (upd && clip) ? clip[1] : 1.0f;
     const int64_t d = T.d;
+    // the step's reg-gradient rows (R.w_lo set, ABI 10): added to the gradient here, from the row's
+    // parameters as the forward read them (before any replay below), instead of by passes after the
+    // backward
+    const bool reg = upd && R.w_lo != nullptr;
+    int64_t nf = 0, nn = 0;
+    if (reg) reg_counts(R, row, nf, nn);
     float4* P = reinterpret_cast<float4*>(trow(T.p_lo, T.p_hi, T.split, row, d)) + l;
     float4* M = reinterpret_cast<float4*>(trow(T.m_lo, T.m_hi, T.split, row, d)) + l;
     float4* V = reinterpret_cast<float4*>(trow(T.v_lo, T.v_hi, T.split, row, d)) + l;
@@ -248,6 +255,11 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
         p[q] = P[q * LPR];
         m[q] = M[q * LPR];
         v[q] = V[q * LPR];
+    }
+    float4 w0[NV];  // (a copy: no wait on the counts before the replays)
+    if (reg) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q) w0[q] = p[q];
     }
     // replays [from, fast_end) in the shortened arithmetic (bitwise the same), the rest in full; a
     // row with fewer than kFastMinReplays to replay skips it (the range checks cost about what two
@@ -284,6 +296,7 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             float4 gv = G[q * LPR];
+            if (reg && (nf > 0 || nn > 0)) gv = reg_apply(gv, w0[q], reg_scale(R.coeff, R.B, T.d), nf, nn);
             adam_elem(p[q].x, gv.x, m[q].x, v[q].x, coef, c.x, c.y, rc, k);
             adam_elem(p[q].y, gv.y, m[q].y, v[q].y, coef, c.x, c.y, rc, k);
             adam_elem(p[q].z, gv.z, m[q].z, v[q].z, coef, c.x, c.y, rc, k);
@@ -305,7 +318,7 @@ __global__ __launch_bounds__(kBlock) void k_row_adam(RowTables T, RowList L, int
 // Sum of squares of the listed (duplicate-free) gradient rows: per-block partials, in a fixed
 // assignment (deterministic), finished by the dense path's k_norm_finish.
 template <int LPR, int NV>
-__global__ __launch_bounds__(kBlock) void k_row_sqnorm(RowTables T, RowList L, float* __restrict__ partial) {
+__global__ __launch_bounds__(kBlock) void k_row_sqnorm(RowTables T, RowList L, float* __restrict__ partial, RegRows R) {
     constexpr int GPB = kBlock / LPR;
     __shared__ float red[kBlock / 64];
     const int g = threadIdx.x / LPR;
@@ -316,9 +329,19 @@ __global__ __launch_bounds__(kBlock) void k_row_sqnorm(RowTables T, RowList L, f
         int64_t row;
         if (!list_row(L, i, row)) continue;
         const float4* G = reinterpret_cast<const float4*>(trow(T.g_lo, T.g_hi, T.split, row, int64_t(T.d))) + l;
+        // the reg rows (ABI 10): the norm of g + them; the counts and W issued beside G
+        int64_t nf = 0, nn = 0;
+        float4 w[NV];
+        if (R.w_lo) {
+            reg_counts(R, row, nf, nn);
+            const float4* W = reinterpret_cast<const float4*>(trow(R.w_lo, R.w_hi, R.w_split, row, int64_t(T.d))) + l;
+#pragma unroll
+            for (int q = 0; q < NV; ++q) w[q] = W[q * LPR];
+        }
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
-            const float4 x = G[q * LPR];
+            float4 x = G[q * LPR];
+            if (R.w_lo) x = reg_apply(x, w[q], reg_scale(R.coeff, R.B, T.d), nf, nn);
             acc += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
         }
     }
@@ -361,19 +384,19 @@ constexpr int kRowNormBlocks = 2048;
 template <int LPR, int NV>
 int launch_row_adam(const RowTables& T, const RowList& L, int64_t n_rows, int32_t* last, int32_t* claim,
                     const int64_t* step, const float4* consts, const AdamK& k, const float* clip, int mode,
-                    hipStream_t s) {
+                    const RegRows& R, hipStream_t s) {
     constexpr int GPB = kBlock / LPR;
     const int64_t n = mode == 2 ? n_rows : L.n_a + L.n_b;
     if (n <= 0) return LGCN_OK;
     k_row_adam<LPR, NV><<<dim3(static_cast<unsigned>((n + GPB - 1) / GPB)), kBlock, 0, s>>>(T, L, n_rows, last, claim,
-                                                                                          step, consts, k, clip, mode);
+                                                                                          step, consts, k, clip, mode, R);
     return check_launch("k_row_adam");
 }
 
 template <int LPR, int NV>
 int launch_row_norm(const RowTables& T, const RowList& L, float max_norm, float* ws, float* out, int64_t* step,
-                    hipStream_t s) {
-    k_row_sqnorm<LPR, NV><<<kRowNormBlocks, kBlock, 0, s>>>(T, L, ws);
+                    const RegRows& R, hipStream_t s) {
+    k_row_sqnorm<LPR, NV><<<kRowNormBlocks, kBlock, 0, s>>>(T, L, ws, R);
     if (int rc = check_launch("k_row_sqnorm")) return rc;
     if (!out) return LGCN_OK;  // partials only (lgcn_row_grad_sqnorm)
     k_norm_finish_rows<<<1, kBlock, 0, s>>>(ws, kRowNormBlocks, max_norm, out, step);
@@ -403,26 +426,12 @@ int check_tables(const RowTables& T, bool need_grad) {
         default: return fail(LGCN_E_UNSUPPORTED, "lgcn_row_adam: d=%d", T.d);     \
     }
 
-}  // namespace
-
-extern "C" {
-
-int lgcn_adam_consts(float* consts, int64_t t0, int64_t t1, float lr, double beta1, double beta2,
-                     lgcn_stream_t stream) {
-    if (!consts || t0 < 1 || t1 < t0) return fail(LGCN_E_ARG, "lgcn_adam_consts: bad range");
-    if (!al16(consts)) return fail(LGCN_E_ARG, "lgcn_adam_consts: consts must be 16-byte aligned");
-    const int64_t n = t1 - t0 + 1;
-    k_adam_consts<<<grid_for(n, kBlock, int64_t(1) << 30), kBlock, 0, as_stream(stream)>>>(
-        reinterpret_cast<float4*>(consts), t0, t1, lr, beta1, beta2);
-    return check_launch("k_adam_consts");
-}
-
-int lgcn_row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_lo, float* m_hi, float* v_lo,
+int row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_lo, float* m_hi, float* v_lo,
                   float* v_hi, int64_t split, int32_t d, const int32_t* rows_a, int64_t n_a, const int64_t* keys_b,
                   int64_t n_b, int64_t off_b, const uint8_t* first_b, const uint8_t* skip_b, int64_t n_rows,
                   int32_t* last, int32_t* claim, int64_t* step, const float* consts, float one_minus_beta1,
                   float beta2, float one_minus_beta2, float eps, const float* clip, int32_t mode,
-                  lgcn_stream_t stream) {
+                  const RegRows& R, lgcn_stream_t stream) {
     RowTables T{p_lo, p_hi, g_lo, g_hi, m_lo, m_hi, v_lo, v_hi, split, d};
     if (int rc = check_tables(T, mode == 1 || mode == 3)) return rc;
     if (mode < 0 || mode > 3 || !last || !step || !consts || (mode == 0 && !claim) || n_a < 0 || n_b < 0 ||
@@ -443,7 +452,7 @@ int lgcn_row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_l
     if (!al16(consts)) return fail(LGCN_E_ARG, "lgcn_row_adam: consts must be 16-byte aligned");
     const auto* c2 = reinterpret_cast<const float4*>(consts);
     int rc = LGCN_OK;
-#define LGCN_RA(LP, NVV) launch_row_adam<LP, NVV>(T, L, n_rows, last, claim, step, c2, k, clip, mode, s)
+#define LGCN_RA(LP, NVV) launch_row_adam<LP, NVV>(T, L, n_rows, last, claim, step, c2, k, clip, mode, R, s)
     auto run = [&]() -> int { LGCN_ROW_DISPATCH(LGCN_RA) };
 #undef LGCN_RA
     rc = run();
@@ -455,12 +464,10 @@ int lgcn_row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_l
     return LGCN_OK;
 }
 
-int lgcn_row_grad_norm_workspace_floats(void) { return kRowNormBlocks; }
-
-int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
+int row_norm(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
                        int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
                        const uint8_t* skip_b, float max_norm, float* ws, float* out, int64_t* step_advance,
-                       lgcn_stream_t stream) {
+                       const RegRows& R, lgcn_stream_t stream) {
     RowTables T{nullptr, nullptr, const_cast<float*>(g_lo), const_cast<float*>(g_hi), nullptr, nullptr, nullptr,
                 nullptr, split, d};
     if (!g_lo || !ws || n_a < 0 || n_b < 0 || (n_a > 0 && !rows_a) || (n_b > 0 && !keys_b))
@@ -468,9 +475,82 @@ int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int3
     if (!al16(g_lo) || (g_hi && !al16(g_hi))) return fail(LGCN_E_UNSUPPORTED, "lgcn_row_grad_norm: alignment");
     RowList L{rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b};
     hipStream_t s = as_stream(stream);
-#define LGCN_RN(LP, NVV) launch_row_norm<LP, NVV>(T, L, max_norm, ws, out, step_advance, s)
+#define LGCN_RN(LP, NVV) launch_row_norm<LP, NVV>(T, L, max_norm, ws, out, step_advance, R, s)
     LGCN_ROW_DISPATCH(LGCN_RN)
 #undef LGCN_RN
+}
+
+
+// lgcn_reg_rows_t -> RegRows, checked (the norm reads W; the update uses its own parameter rows)
+int to_reg(const lgcn_reg_rows_t* r, int32_t d, RegRows& R, const char* who) {
+    if (!r || !r->w_lo || r->B < 1 || r->neg_off < 0 || r->neg_rows < 0 ||
+        (r->neg_rows > 0 && (r->neg_rowptr == nullptr) == (r->neg_count == nullptr)))
+        return fail(LGCN_E_ARG, "%s: bad reg rows (w_lo, B >= 1, and exactly one of neg_rowptr / neg_count "
+                    "when neg_rows > 0)", who);
+    if (!al16(r->w_lo) || (r->w_hi && !al16(r->w_hi)) || d % 4 != 0)
+        return fail(LGCN_E_UNSUPPORTED, "%s: reg tables must be 16-byte aligned", who);
+    R = RegRows{r->w_lo, r->w_hi, r->w_split, r->coeff, r->B, r->fixed_rowptr, r->neg_rowptr, r->neg_count,
+                r->neg_off, r->neg_rows};
+    return LGCN_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lgcn_adam_consts(float* consts, int64_t t0, int64_t t1, float lr, double beta1, double beta2,
+                     lgcn_stream_t stream) {
+    if (!consts || t0 < 1 || t1 < t0) return fail(LGCN_E_ARG, "lgcn_adam_consts: bad range");
+    if (!al16(consts)) return fail(LGCN_E_ARG, "lgcn_adam_consts: consts must be 16-byte aligned");
+    const int64_t n = t1 - t0 + 1;
+    k_adam_consts<<<grid_for(n, kBlock, int64_t(1) << 30), kBlock, 0, as_stream(stream)>>>(
+        reinterpret_cast<float4*>(consts), t0, t1, lr, beta1, beta2);
+    return check_launch("k_adam_consts");
+}
+
+int lgcn_row_adam(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_lo, float* m_hi, float* v_lo,
+                  float* v_hi, int64_t split, int32_t d, const int32_t* rows_a, int64_t n_a, const int64_t* keys_b,
+                  int64_t n_b, int64_t off_b, const uint8_t* first_b, const uint8_t* skip_b, int64_t n_rows,
+                  int32_t* last, int32_t* claim, int64_t* step, const float* consts, float one_minus_beta1,
+                  float beta2, float one_minus_beta2, float eps, const float* clip, int32_t mode,
+                  lgcn_stream_t stream) {
+    return row_adam(p_lo, p_hi, g_lo, g_hi, m_lo, m_hi, v_lo, v_hi, split, d, rows_a, n_a, keys_b, n_b, off_b, first_b,
+                    skip_b, n_rows, last, claim, step, consts, one_minus_beta1, beta2, one_minus_beta2, eps, clip, mode,
+                    RegRows{}, stream);
+}
+
+int lgcn_row_adam_reg(float* p_lo, float* p_hi, float* g_lo, float* g_hi, float* m_lo, float* m_hi, float* v_lo,
+                      float* v_hi, int64_t split, int32_t d, const int32_t* rows_a, int64_t n_a, const int64_t* keys_b,
+                      int64_t n_b, int64_t off_b, const uint8_t* first_b, const uint8_t* skip_b, int32_t* last,
+                      int64_t* step, const float* consts, float one_minus_beta1, float beta2, float one_minus_beta2,
+                      float eps, const float* clip, int32_t mode, const lgcn_reg_rows_t* reg, lgcn_stream_t stream) {
+    RegRows R{};
+    if (int rc = to_reg(reg, d, R, "lgcn_row_adam_reg")) return rc;
+    if (mode != 1 && mode != 3) return fail(LGCN_E_ARG, "lgcn_row_adam_reg: mode 1 or 3 (an update)");
+    return row_adam(p_lo, p_hi, g_lo, g_hi, m_lo, m_hi, v_lo, v_hi, split, d, rows_a, n_a, keys_b, n_b, off_b, first_b,
+                    skip_b, 0, last, nullptr, step, consts, one_minus_beta1, beta2, one_minus_beta2, eps, clip, mode, R,
+                    stream);
+}
+
+int lgcn_row_grad_norm_workspace_floats(void) { return kRowNormBlocks; }
+
+int lgcn_row_grad_norm(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
+                       int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
+                       const uint8_t* skip_b, float max_norm, float* ws, float* out, int64_t* step_advance,
+                       lgcn_stream_t stream) {
+    return row_norm(g_lo, g_hi, split, d, rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b, max_norm, ws, out,
+                    step_advance, RegRows{}, stream);
+}
+
+int lgcn_row_grad_norm_reg(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,
+                           int64_t n_a, const int64_t* keys_b, int64_t n_b, int64_t off_b, const uint8_t* first_b,
+                           const uint8_t* skip_b, float max_norm, float* ws, float* out, int64_t* step_advance,
+                           const lgcn_reg_rows_t* reg, lgcn_stream_t stream) {
+    RegRows R{};
+    if (int rc = to_reg(reg, d, R, "lgcn_row_grad_norm_reg")) return rc;
+    if (!out) return fail(LGCN_E_ARG, "lgcn_row_grad_norm_reg: null out");
+    return row_norm(g_lo, g_hi, split, d, rows_a, n_a, keys_b, n_b, off_b, first_b, skip_b, max_norm, ws, out,
+                    step_advance, R, stream);
 }
 
 int lgcn_row_grad_sqnorm(const float* g_lo, const float* g_hi, int64_t split, int32_t d, const int32_t* rows_a,

@@ -25,7 +25,7 @@ E_ARG, E_WORKSPACE, E_UNSUPPORTED = -1, -2, -3  # include/lgcn.h LGCN_E_*
 
 ITEM_BYTES = 16   # lgcn_item_t {int64 beg; int32 len; int32 dst}
 SPLIT_BYTES = 16  # lgcn_split_t {int32 row, pbeg, pcnt, pad}
-ABI_VERSION = 9  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
+ABI_VERSION = 10  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
 DIGEST_BLOCKS = 1024  # LGCN_DIGEST_BLOCKS
 
 _lib = None
@@ -93,6 +93,8 @@ _SIGS = {
     "lgcn_range_scatter_add_loss": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp,
                                      _i64, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _vp, _vp],
                                     ctypes.c_int),
+    "lgcn_range_scatter_add_counts": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp,
+                                       _vp, _vp, _i64, _i32, _f32, _vp, _vp], ctypes.c_int),
     "lgcn_sorted_scatter_add": ([_vp, _vp, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _i64,
                                  _f32, _i64, _vp, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_grouped_reg_add": ([_vp, _i64, _i64, _vp, _vp, _i64, _i32, _f32, _i64, _vp, _vp, _i64, _vp], ctypes.c_int),
@@ -100,6 +102,10 @@ _SIGS = {
     "lgcn_adam_consts": ([_vp, _i64, _i64, _f32, ctypes.c_double, ctypes.c_double, _vp], ctypes.c_int),
     "lgcn_row_adam": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64,
                        _vp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _i32, _vp], ctypes.c_int),
+    "lgcn_row_adam_reg": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp,
+                           _vp, _vp, _vp, _f32, _f32, _f32, _f32, _vp, _i32, _vp, _vp], ctypes.c_int),
+    "lgcn_row_grad_norm_reg": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp,
+                                _vp], ctypes.c_int),
     "lgcn_row_grad_norm_workspace_floats": ([], ctypes.c_int),
     "lgcn_row_grad_norm": ([_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp],
                            ctypes.c_int),
@@ -169,6 +175,14 @@ class Tuning(ctypes.Structure):
                 ("reserved", ctypes.c_int32 * 10)]
 
 
+class RegRows(ctypes.Structure):
+    """lgcn_reg_rows_t (include/lgcn.h, ABI 10): a step's reg-gradient rows by occurrence counts."""
+    _fields_ = [("w_lo", ctypes.c_void_p), ("w_hi", ctypes.c_void_p), ("w_split", ctypes.c_int64),
+                ("coeff", ctypes.c_float), ("B", ctypes.c_int64), ("fixed_rowptr", ctypes.c_void_p),
+                ("neg_rowptr", ctypes.c_void_p), ("neg_count", ctypes.c_void_p), ("neg_off", ctypes.c_int64),
+                ("neg_rows", ctypes.c_int64)]
+
+
 class LgcnError(RuntimeError):
     pass
 
@@ -204,7 +218,7 @@ INCLUDE = _HERE.parent.parent / "include"
 SOURCES = ("lgcn_plan.hip", "lgcn_spmm.hip", "lgcn_optim.hip", "lgcn_bpr.hip", "lgcn_recall.hip", "lgcn_rowadam.hip",
            "lgcn_exchange.hip", "lgcn_partition.cpp", "lgcn_sample.cpp", "lgcn_tuning.cpp")
 # the headers they include (csrc/), hashed and tracked as build dependencies with include/lgcn.h
-HEADERS = ("lgcn_common.h", "lgcn_exact.h")
+HEADERS = ("lgcn_common.h", "lgcn_exact.h", "lgcn_reg.h")
 
 
 def source_sha256() -> str:

@@ -162,11 +162,18 @@ class RowLazyAdam:
         return (*p, *g, self.m[0].data_ptr(), self.m[1].data_ptr(), self.v[0].data_ptr(), self.v[1].data_ptr(),
                 self.U, self.d)
 
-    def _row_adam(self, rows_a, keys_b, off_b, first_b, skip_b, n_rows, clip, mode):
+    def _row_adam(self, rows_a, keys_b, off_b, first_b, skip_b, n_rows, clip, mode, reg=None):
         lib = _ffi.load()
         b1, b2 = self.betas
         na = rows_a.numel() if rows_a is not None else 0
         nb = keys_b.numel() if keys_b is not None else 0
+        if reg is not None:  # the update over g + the step's reg rows (mode 1 / 3)
+            _ffi.check(lib.lgcn_row_adam_reg(*self._tables(True), _ffi.ptr(rows_a), na, _ffi.ptr(keys_b), nb, off_b,
+                                             _ffi.ptr(first_b), _ffi.ptr(skip_b), self.last.data_ptr(),
+                                             self.step_dev.data_ptr(), self.consts.data_ptr(), 1 - b1, b2, 1 - b2,
+                                             self.eps, _ffi.ptr(clip), mode, ctypes.byref(reg),
+                                             _ffi.stream_of(self.device)), "lgcn_row_adam_reg")
+            return
         _ffi.check(lib.lgcn_row_adam(*self._tables(mode in (1, 3)), _ffi.ptr(rows_a), na, _ffi.ptr(keys_b), nb, off_b,
                                      _ffi.ptr(first_b), _ffi.ptr(skip_b), n_rows, self.last.data_ptr(),
                                      self.claim.data_ptr(), self.step_dev.data_ptr(), self.consts.data_ptr(),
@@ -212,16 +219,20 @@ class RowLazyAdam:
 
     def step_rows(self, rows_a: torch.Tensor | None, keys_b: torch.Tensor | None = None, off_b: int = 0,
                   first_b: torch.Tensor | None = None, skip_b: torch.Tensor | None = None,
-                  gather_partials=None) -> None:
+                  gather_partials=None, reg: _ffi.RegRows | None = None) -> None:
         """One Adam step whose gradient (self.gu / self.gi) is zero outside the listed rows, which
         must be duplicate-free (first_b / skip_b filter list b): clip norm over them, then the
         update; rows not listed are deferred. gather_partials (column-sharded training: each rank
         holds some columns of every row): called with this rank's norm block partials, returns
-        every rank's partials in rank order — the norm is finished over all of them."""
+        every rank's partials in rank order — the norm is finished over all of them.
+        reg (lgcn_reg_rows_t): the gradient is g + the step's BPR reg rows, formed by the norm and
+        the update from their occurrence counts (g itself is not written)."""
         if self.steps + 1 > self.max_steps:
             raise RuntimeError(f"RowLazyAdam: more than max_steps={self.max_steps} steps")
         lib = _ffi.load()
         clip = None
+        if reg is not None and gather_partials is not None:
+            raise ValueError("step_rows: reg rows are formed for whole rows (no column partials)")
         if self.max_grad_norm is not None and gather_partials is not None:
             na = rows_a.numel() if rows_a is not None else 0
             nb = keys_b.numel() if keys_b is not None else 0
@@ -242,16 +253,18 @@ class RowLazyAdam:
         if self.max_grad_norm is not None:
             na = rows_a.numel() if rows_a is not None else 0
             nb = keys_b.numel() if keys_b is not None else 0
-            _ffi.check(lib.lgcn_row_grad_norm(self.gu.data_ptr(), self.gi.data_ptr(), self.U, self.d,
-                                              _ffi.ptr(rows_a), na, _ffi.ptr(keys_b), nb, off_b, _ffi.ptr(first_b),
-                                              _ffi.ptr(skip_b), float(self.max_grad_norm), self.norm_ws.data_ptr(),
-                                              self.last_norm.data_ptr(), self.step_dev.data_ptr(),
-                                              _ffi.stream_of(self.device)),
-                       "lgcn_row_grad_norm")
+            args = (self.gu.data_ptr(), self.gi.data_ptr(), self.U, self.d, _ffi.ptr(rows_a), na, _ffi.ptr(keys_b), nb,
+                    off_b, _ffi.ptr(first_b), _ffi.ptr(skip_b), float(self.max_grad_norm), self.norm_ws.data_ptr(),
+                    self.last_norm.data_ptr(), self.step_dev.data_ptr())
+            if reg is not None:
+                _ffi.check(lib.lgcn_row_grad_norm_reg(*args, ctypes.byref(reg), _ffi.stream_of(self.device)),
+                           "lgcn_row_grad_norm_reg")
+            else:
+                _ffi.check(lib.lgcn_row_grad_norm(*args, _ffi.stream_of(self.device)), "lgcn_row_grad_norm")
             clip = self.last_norm
         # with the clip norm, its finishing launch also advances the device step counter (mode 3:
         # one launch fewer per step); without it the update advances it itself (mode 1)
-        self._row_adam(rows_a, keys_b, off_b, first_b, skip_b, 0, clip, 1 if clip is None else 3)
+        self._row_adam(rows_a, keys_b, off_b, first_b, skip_b, 0, clip, 1 if clip is None else 3, reg)
         self.steps += 1
 
     def flush(self) -> None:

@@ -228,6 +228,9 @@ class _BatchState:
             self.c2buf = torch.empty((B if self.neg_rowptr is None else 1, d), dtype=torch.float32, device=dev)
             self.c2flag = torch.empty(B, dtype=torch.uint8, device=dev)
             self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+            # the range scatter's per-row key counts when the reg rows are formed in the update
+            # (lgcn_range_scatter_add_counts; the sorted path counts by neg_rowptr)
+            self.neg_count = torch.empty(max(1, I), dtype=torch.int32, device=dev) if self.neg_rowptr is None else None
         self.cf = torch.empty((3 * B, d), dtype=torch.float32, device=dev)
         # reg-gradient rows: materialised only for the large-batch sort path; the segment-plan path
         # forms their sums from the layer-0 rows (lgcn_reg_rows_add, the scatters' reg source)
@@ -271,14 +274,24 @@ def loss_fused(st, I: int, cols=None) -> bool:
 
 
 def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: float, store_unless, stream,
-                      uw, iw, coeff: float, loss=None) -> None:
+                      uw, iw, coeff: float, loss=None, counts: bool = False) -> None:
     """dF rows of the step's negatives into the gradient tables and the first-occurrence flags
     (st.c2flag); the range scatter also parks each row's reg-rows sum (formed from the layer-0
-    rows uw / iw) in its first-occurrence slot for add_negative_reg_rows after the backward.
+    rows uw / iw) in its first-occurrence slot for add_negative_reg_rows after the backward — or,
+    counts=True (the reg rows formed in the update), writes each row's key count to st.neg_count.
     loss = (terms, d, coeff, out): the step's loss sum in the same launch (loss_fused)."""
     B = st.B
     C = st.cf[2 * B:]
     reg = (None, uw.data_ptr(), iw.data_ptr(), U, coeff, B)
+    if st.neg_rowptr is None and counts:
+        terms, ld, lcoeff, out = loss if loss is not None else (None, 0, 0.0, None)
+        _ffi.check(lib.lgcn_range_scatter_add_counts(st.neg.data_ptr(), B, I, U, C.data_ptr(), d, gu.data_ptr(),
+                                                     gi.data_ptr(), U, mul, div, st.c2flag.data_ptr(),
+                                                     st.overflow.data_ptr(), _ffi.ptr(store_unless),
+                                                     st.neg_count.data_ptr(), _ffi.ptr(terms),
+                                                     B if terms is not None else 0, ld, lcoeff, _ffi.ptr(out), stream),
+                   "lgcn_range_scatter_add_counts")
+        return
     if st.neg_rowptr is None:
         common = (st.neg.data_ptr(), B, I, U, C.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U, mul, div, *reg,
                   st.c2buf.data_ptr(), st.c2flag.data_ptr(), st.overflow.data_ptr(), _ffi.ptr(store_unless))
@@ -395,6 +408,11 @@ class FusedTrainStep:
         if loss_acc is not None and (loss_acc.dtype != torch.float64 or loss_acc.numel() < 1 or not lazy):
             raise ValueError("loss_acc must be a device float64 tensor of >= 1 element (lazy=True)")
         self.loss_acc = loss_acc
+        # one GPU, whole rows: the BPR reg-gradient rows go into the clip norm and the update
+        # (lgcn_row_*_reg) instead of two passes after the backward — bitwise the same step
+        from . import tuning
+
+        self.reg_in_update = bool(lazy and exchange is None and cols is None and tuning.get().reg_in_update)
         self._gen = None
         self._k = 0  # steps taken (the index of the next step)
         self._owner_graphs = None
@@ -571,10 +589,12 @@ class FusedTrainStep:
                  stream=stream)
             # ... the negatives' rows added (stored where the row is outside the touched set)
             scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream, uw, iw, reg_coeff,
-                              (st.terms, d, self.coeff, st.loss) if loss_fused(st, I, self.cols) else None)
+                              (st.terms, d, self.coeff, st.loss) if loss_fused(st, I, self.cols) else None,
+                              counts=self.reg_in_update)
             propagate_backward_seeded(gu, gi, st.plan, K)
-            add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, reg_coeff, stream)
-            add_negative_reg_rows(lib, st, gu, gi, U, d, uw, iw, reg_coeff, stream)
+            if not self.reg_in_update:  # else _lazy_update's norm and update form them (_reg_rows)
+                add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, reg_coeff, stream)
+                add_negative_reg_rows(lib, st, gu, gi, U, d, uw, iw, reg_coeff, stream)
             ex = self.exchange
             if self.owner:
                 # this rank's rows with a possibly nonzero gradient -> their owners' blocks
@@ -601,6 +621,20 @@ class FusedTrainStep:
                                                     stream), "lgcn_loss_accumulate")
         return st.loss
 
+    def _reg_rows(self, st: _BatchState):
+        """The step's BPR reg-gradient rows by occurrence counts (lgcn_reg_rows_t): the fixed
+        (user, positive) counts from the batch's segment plan, the negatives' from the sorted path's
+        grouping or the range scatter's st.neg_count; kreg = coeff * 2 / (B * d) from the tables."""
+        if st.B == 0:
+            return None
+        m = self.model
+        U = m.num_users
+        return _ffi.RegRows(w_lo=m.user_embedding.weight.data_ptr(), w_hi=m.item_embedding.weight.data_ptr(),
+                            w_split=U, coeff=self.coeff, B=st.B, fixed_rowptr=st.fixed_sparse.rowptr.data_ptr(),
+                            neg_rowptr=_ffi.ptr(st.neg_rowptr),
+                            neg_count=None if st.neg_rowptr is not None else st.neg_count.data_ptr(),
+                            neg_off=U, neg_rows=m.num_items)
+
     def _lazy_update(self, st: _BatchState) -> None:
         """Clip + Adam on the rows whose gradient can be nonzero: this rank's (touched rows, then
         negatives at their first occurrence that are not touched), or with an exchange the union
@@ -611,7 +645,8 @@ class FusedTrainStep:
             if ex is None:
                 opt.step_rows(st.touched_rows, st.neg, self.model.num_users, first_b=st.c2flag,
                               skip_b=st.plan.touched,
-                              gather_partials=self.cols.gather_partials if self.cols is not None else None)
+                              gather_partials=self.cols.gather_partials if self.cols is not None else None,
+                              reg=self._reg_rows(st) if self.reg_in_update else None)
                 return
             lib = _ffi.load()
             m = self.model

@@ -51,6 +51,9 @@ class Tuning:
     recall_ties: str = "index"
     # utils.train_test.train routes eligible calls to the fused batch step (False: reference loop)
     harness_fused: bool = True
+    # single-GPU lazy step: the BPR reg-gradient rows formed inside the clip norm and the Adam update
+    # from their occurrence counts (lgcn_row_*_reg, bitwise) instead of two passes after the backward
+    reg_in_update: bool = True
     # run the exchanges' RCCL branches even on a gloo group (tests: gloo carries the bytes)
     device_collectives: bool = False
     # --- native (lgcn_tuning_t) -----------------------------------------------------------------

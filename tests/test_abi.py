@@ -44,7 +44,7 @@ def test_abi_version_and_error_codes():
     from lgcn_amd import _ffi
 
     lib = _ffi.load()
-    assert lib.lgcn_abi_version() == _ffi.ABI_VERSION == 9
+    assert lib.lgcn_abi_version() == _ffi.ABI_VERSION == 10
     b = ctypes.c_size_t(0)
     assert lib.lgcn_csr_workspace_size(-1, 5, ctypes.byref(b)) == -1
     assert b"bad args" in lib.lgcn_last_error()
