@@ -527,12 +527,13 @@ typedef struct {
 /* lgcn_range_scatter_add for the reg rows' counted form (ABI 10): no second source, no parked sum;
  * instead reg_count[r] (int32[nrows], every row written) = the number of keys of row r, and c2flag as
  * always. terms (nullable): with loss / loss_B / loss_d / loss_coeff, the step's loss as
- * lgcn_range_scatter_add_loss sums it. */
+ * lgcn_range_scatter_add_loss sums it; loss_acc (nullable, needs terms): then also
+ * loss_acc[0] += (double)loss[0] * loss_w in the same workgroup, as lgcn_loss_accumulate adds it. */
 int lgcn_range_scatter_add_counts(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
                                   int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
                                   uint8_t* c2flag, int32_t* overflow, const uint8_t* store_unless, int32_t* reg_count,
                                   const float* terms, int64_t loss_B, int32_t loss_d, float loss_coeff, float* loss,
-                                  lgcn_stream_t stream);
+                                  double* loss_acc, double loss_w, lgcn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Row-lazy Adam (lgcn_rowadam.hip) for the sparse batch step: exact replay of the zero-gradient

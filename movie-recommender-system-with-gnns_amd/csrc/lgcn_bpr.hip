@@ -200,7 +200,8 @@ constexpr int kLossPartBlock = 256;
 // loss of B triplets. Run as its own launch (k_bpr_loss) or as the extra workgroup of the range
 // scatter (k_range_scatter has the same block size): the same association either way.
 __device__ __forceinline__ void bpr_loss_block(const float* __restrict__ t, int64_t n, int64_t stride, int64_t B,
-                                               int32_t d, float coeff, float* __restrict__ loss) {
+                                               int32_t d, float coeff, float* __restrict__ loss,
+                                               double* __restrict__ acc = nullptr, double w = 0.0) {
     __shared__ float r0[kLossBlock / 64], r1[kLossBlock / 64];
     float s0 = 0.f, s1 = 0.f;
     constexpr int kU = 8;
@@ -239,7 +240,12 @@ __device__ __forceinline__ void bpr_loss_block(const float* __restrict__ t, int6
         }
         const float bf = static_cast<float>(B);
         // -(mean softplus) / 10 + coeff * mean(squares); B == 0 gives NaN, as torch's empty mean
-        loss[0] = -((a / bf) / 10.0f) + coeff * (c / (bf * static_cast<float>(d)));
+        const float l = -((a / bf) / 10.0f) + coeff * (c / (bf * static_cast<float>(d)));
+        loss[0] = l;
+        if (acc) {  // the harness's epoch sum, as k_loss_accumulate adds it (ABI 10)
+            const double cw = static_cast<double>(l) * w;
+            acc[0] = acc[0] + cw;
+        }
     }
 }
 
@@ -255,6 +261,8 @@ struct LossArgs {
     int32_t d;
     float coeff;
     float* loss;
+    double* acc;  // nullable: acc[0] += double(loss) * w in the same workgroup
+    double w;
 };
 
 // First stage of the two-stage sum: block p sums its contiguous share of each term array (threads
@@ -372,7 +380,7 @@ __global__ __launch_bounds__(kRSBlock) void k_range_scatter(const int64_t* __res
                                                             int32_t* __restrict__ reg_count, LossArgs la) {
     static_assert(kRSBlock == kLossBlock, "the loss workgroup needs the loss block's size (its association)");
     if (la.loss != nullptr && blockIdx.x == gridDim.x - 1) {
-        bpr_loss_block(la.terms, la.B, la.B, la.B, la.d, la.coeff, la.loss);
+        bpr_loss_block(la.terms, la.B, la.B, la.B, la.d, la.coeff, la.loss, la.acc, la.w);
         return;
     }
     constexpr int GPB = kRSBlock / LPR;
@@ -865,7 +873,7 @@ int lgcn_range_scatter_add(const int64_t* keys, int64_t B, int64_t nrows, int64_
                            const uint8_t* store_unless, lgcn_stream_t stream) {
     return range_scatter(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg_w_lo, reg_w_hi,
                          reg_w_split, reg_coeff, reg_B, c2buf, c2flag, overflow, store_unless, nullptr,
-                         LossArgs{nullptr, 0, 0, 0.f, nullptr}, stream);
+                         LossArgs{nullptr, 0, 0, 0.f, nullptr, nullptr, 0.0}, stream);
 }
 
 int lgcn_range_scatter_add_loss(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
@@ -879,21 +887,23 @@ int lgcn_range_scatter_add_loss(const int64_t* keys, int64_t B, int64_t nrows, i
                     "1 <= B < %d, and a scatter with work)", (long long)loss_B, LGCN_LOSS_FUSED_MAX_B);
     return range_scatter(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, C2, reg_w_lo, reg_w_hi,
                          reg_w_split, reg_coeff, reg_B, c2buf, c2flag, overflow, store_unless, nullptr,
-                         LossArgs{terms, loss_B, loss_d, loss_coeff, loss}, stream);
+                         LossArgs{terms, loss_B, loss_d, loss_coeff, loss, nullptr, 0.0}, stream);
 }
 
 int lgcn_range_scatter_add_counts(const int64_t* keys, int64_t B, int64_t nrows, int64_t key_offset, const float* C,
                                   int32_t d, float* out_lo, float* out_hi, int64_t split, float mul, float div,
                                   uint8_t* c2flag, int32_t* overflow, const uint8_t* store_unless, int32_t* reg_count,
                                   const float* terms, int64_t loss_B, int32_t loss_d, float loss_coeff, float* loss,
-                                  lgcn_stream_t stream) {
+                                  double* loss_acc, double loss_w, lgcn_stream_t stream) {
     if (!c2flag || !reg_count) return fail(LGCN_E_ARG, "lgcn_range_scatter_add_counts: null c2flag / reg_count");
-    if (terms && (!loss || loss_B < 1 || loss_d <= 0 || loss_B >= LGCN_LOSS_FUSED_MAX_B || B <= 0 || nrows <= 0))
+    if ((loss_acc && !terms) ||
+        (terms && (!loss || loss_B < 1 || loss_d <= 0 || loss_B >= LGCN_LOSS_FUSED_MAX_B || B <= 0 || nrows <= 0)))
         return fail(LGCN_E_ARG, "lgcn_range_scatter_add_counts: bad loss args (B=%lld; the single-block sum needs "
                     "1 <= B < %d, and a scatter with work)", (long long)loss_B, LGCN_LOSS_FUSED_MAX_B);
     return range_scatter(keys, B, nrows, key_offset, C, d, out_lo, out_hi, split, mul, div, nullptr, nullptr, nullptr,
                          0, 0.f, 0, nullptr, c2flag, overflow, store_unless, reg_count,
-                         terms ? LossArgs{terms, loss_B, loss_d, loss_coeff, loss} : LossArgs{nullptr, 0, 0, 0.f, nullptr},
+                         terms ? LossArgs{terms, loss_B, loss_d, loss_coeff, loss, loss_acc, loss_w}
+                               : LossArgs{nullptr, 0, 0, 0.f, nullptr, nullptr, 0.0},
                          stream);
 }
 

@@ -94,7 +94,7 @@ _SIGS = {
                                      _i64, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _vp, _vp],
                                     ctypes.c_int),
     "lgcn_range_scatter_add_counts": ([_vp, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp,
-                                       _vp, _vp, _i64, _i32, _f32, _vp, _vp], ctypes.c_int),
+                                       _vp, _vp, _i64, _i32, _f32, _vp, _vp, ctypes.c_double, _vp], ctypes.c_int),
     "lgcn_sorted_scatter_add": ([_vp, _vp, _i64, _i64, _vp, _i32, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _i64,
                                  _f32, _i64, _vp, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_grouped_reg_add": ([_vp, _i64, _i64, _vp, _vp, _i64, _i32, _f32, _i64, _vp, _vp, _i64, _vp], ctypes.c_int),

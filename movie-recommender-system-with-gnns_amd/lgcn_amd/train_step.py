@@ -274,24 +274,29 @@ def loss_fused(st, I: int, cols=None) -> bool:
 
 
 def scatter_negatives(lib, st, gu, gi, U: int, I: int, d: int, mul: float, div: float, store_unless, stream,
-                      uw, iw, coeff: float, loss=None, counts: bool = False) -> None:
+                      uw, iw, coeff: float, loss=None, counts: bool = False, loss_acc=None) -> None:
     """dF rows of the step's negatives into the gradient tables and the first-occurrence flags
     (st.c2flag); the range scatter also parks each row's reg-rows sum (formed from the layer-0
     rows uw / iw) in its first-occurrence slot for add_negative_reg_rows after the backward — or,
     counts=True (the reg rows formed in the update), writes each row's key count to st.neg_count.
-    loss = (terms, d, coeff, out): the step's loss sum in the same launch (loss_fused)."""
+    loss = (terms, d, coeff, out): the step's loss sum in the same launch (loss_fused); loss_acc =
+    (acc, w) with counts and loss: acc[0] += double(loss) * w there too (the harness's epoch sum)."""
     B = st.B
     C = st.cf[2 * B:]
     reg = (None, uw.data_ptr(), iw.data_ptr(), U, coeff, B)
     if st.neg_rowptr is None and counts:
         terms, ld, lcoeff, out = loss if loss is not None else (None, 0, 0.0, None)
+        acc, w = loss_acc if loss_acc is not None else (None, 0.0)
         _ffi.check(lib.lgcn_range_scatter_add_counts(st.neg.data_ptr(), B, I, U, C.data_ptr(), d, gu.data_ptr(),
                                                      gi.data_ptr(), U, mul, div, st.c2flag.data_ptr(),
                                                      st.overflow.data_ptr(), _ffi.ptr(store_unless),
                                                      st.neg_count.data_ptr(), _ffi.ptr(terms),
-                                                     B if terms is not None else 0, ld, lcoeff, _ffi.ptr(out), stream),
+                                                     B if terms is not None else 0, ld, lcoeff, _ffi.ptr(out),
+                                                     _ffi.ptr(acc), float(w), stream),
                    "lgcn_range_scatter_add_counts")
         return
+    if loss_acc is not None:
+        raise ValueError("scatter_negatives: loss_acc needs the counted range scatter with the fused loss")
     if st.neg_rowptr is None:
         common = (st.neg.data_ptr(), B, I, U, C.data_ptr(), d, gu.data_ptr(), gi.data_ptr(), U, mul, div, *reg,
                   st.c2buf.data_ptr(), st.c2flag.data_ptr(), st.overflow.data_ptr(), _ffi.ptr(store_unless))
@@ -588,9 +593,13 @@ class FusedTrainStep:
             spmm(st.fixed_touched, N, d, (st.cf, None, big), None, grads, None, _ffi.EPI_SCALE, div, mul,
                  stream=stream)
             # ... the negatives' rows added (stored where the row is outside the touched set)
+            fused = loss_fused(st, I, self.cols)
+            # the harness's epoch-loss sum rides in the same workgroup as the fused loss (counted
+            # range scatter), else lgcn_loss_accumulate at the end of the step
+            acc_fused = self.loss_acc is not None and fused and self.reg_in_update
             scatter_negatives(lib, st, gu, gi, U, I, d, mul, div, st.plan.touched, stream, uw, iw, reg_coeff,
-                              (st.terms, d, self.coeff, st.loss) if loss_fused(st, I, self.cols) else None,
-                              counts=self.reg_in_update)
+                              (st.terms, d, self.coeff, st.loss) if fused else None, counts=self.reg_in_update,
+                              loss_acc=(self.loss_acc, float(st.n_edges)) if acc_fused else None)
             propagate_backward_seeded(gu, gi, st.plan, K)
             if not self.reg_in_update:  # else _lazy_update's norm and update form them (_reg_rows)
                 add_fixed_reg_rows(lib, st, gu, gi, U, N, d, uw, iw, reg_coeff, stream)
@@ -616,7 +625,7 @@ class FusedTrainStep:
                                               st.touched_rows.numel(), st.neg.data_ptr(), B, U,
                                               st.c2flag.data_ptr(), st.plan.touched.data_ptr(), ex.cap,
                                               ex.ids.data_ptr(), ex.rows.data_ptr(), stream), "lgcn_rows_pack")
-            if self.loss_acc is not None:
+            if self.loss_acc is not None and not acc_fused:
                 _ffi.check(lib.lgcn_loss_accumulate(st.loss.data_ptr(), float(st.n_edges), self.loss_acc.data_ptr(),
                                                     stream), "lgcn_loss_accumulate")
         return st.loss

@@ -257,6 +257,27 @@ def test_harness_fresh_tensors_each_epoch_replay(gpu, tune):
     assert mem[1] == mem[2] == mem[3], mem
 
 
+def test_harness_reg_rows_in_update_bitwise(gpu, tune):
+    """ABI 10: the harness step with the BPR reg rows formed in the clip norm and the update, and its
+    epoch-loss sum riding in the fused loss's workgroup (lgcn_range_scatter_add_counts), is bitwise
+    the step with the two reg passes and its own lgcn_loss_accumulate launch: epoch losses and
+    tables over 3 epochs of the golden batches."""
+    tune(harness_fused=True)
+    G = np.load(GOLDEN / "harness.npz")
+    U, I = int(G["train_U"]), int(G["train_I"])
+    init = (torch.from_numpy(G["train_init_user_w"]), torch.from_numpy(G["train_init_item_w"]))
+    same = [_Batch(torch.from_numpy(G[f"train_batch{p}"])) for p in range(3)]
+    out = {}
+    for flag in (False, True):
+        tune(reg_in_update=flag)
+        losses, w, fast, _ = _epochs(gpu, U, I, init, same, 3)
+        assert fast.step.reg_in_update == flag
+        out[flag] = (losses, w)
+    assert out[False][0] == out[True][0], out
+    for a, b in zip(out[False][1], out[True][1]):
+        assert torch.equal(a, b)
+
+
 def test_harness_one_shot_loader_falls_back_mid_epoch(gpu, tune):
     """a non-bipartite batch after fused steps hands the rest of the epoch to the
     reference loop — the fused steps' Adam state written back first, no batch lost from a one-shot
