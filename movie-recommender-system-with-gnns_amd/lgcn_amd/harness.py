@@ -147,8 +147,11 @@ class _Fast:
         for i, p in enumerate((uw, iw)):
             st = optimizer.state.get(p, {})
             if "exp_avg" in st:
-                self.opt.m[i].copy_(st["exp_avg"])
-                self.opt.v[i].copy_(st["exp_avg_sq"])
+                # the torch state holds these very tables after a store (aliased): nothing to copy
+                if st["exp_avg"] is not self.opt.m[i]:
+                    self.opt.m[i].copy_(st["exp_avg"])
+                if st["exp_avg_sq"] is not self.opt.v[i]:
+                    self.opt.v[i].copy_(st["exp_avg_sq"])
                 s = int(float(st["step"]))
             else:
                 self.opt.m[i].zero_()
@@ -162,17 +165,17 @@ class _Fast:
         self.opt.last.fill_(steps)  # every row current at that step
 
     def store_state(self, optimizer) -> None:
-        """Every row replayed up to date, the moments and step count written back."""
+        """Every row replayed up to date, the moments and step count written back. The torch
+        state's moments ARE the row-lazy optimizer's tables (set once, aliased): no per-epoch copy
+        either way, and a torch Adam step on them (the reference loop between fused epochs)
+        updates them in place. A state replaced from outside (load_state_dict) is copied from."""
         self.step.sync()
         uw, iw = self.model.user_embedding.weight, self.model.item_embedding.weight
         for i, p in enumerate((uw, iw)):
             st = optimizer.state[p]
-            if "exp_avg" in st and st["exp_avg"].shape == p.shape:
-                st["exp_avg"].copy_(self.opt.m[i])
-                st["exp_avg_sq"].copy_(self.opt.v[i])
-            else:
-                st["exp_avg"] = self.opt.m[i].clone(memory_format=torch.preserve_format)
-                st["exp_avg_sq"] = self.opt.v[i].clone(memory_format=torch.preserve_format)
+            for key, t in (("exp_avg", self.opt.m[i]), ("exp_avg_sq", self.opt.v[i])):
+                if st.get(key) is not t:
+                    st[key] = t
             st["step"] = torch.tensor(float(self.opt.steps), dtype=torch.float32)
 
 

@@ -92,6 +92,49 @@ def test_range_scatter_matches_sequential(gpu, B, nrows, d):
     np.testing.assert_array_equal(np.nonzero(flag)[0], firsts)
 
 
+@pytest.mark.parametrize("B,nrows,d,bad", [(1000, 500, 64, False), (10000, 59047, 128, True), (30000, 5000, 64, False),
+                                           (4000, 300000, 32, True), (3000, 10, 64, False)])
+def test_range_scatter_counts(gpu, B, nrows, d, bad):
+    """lgcn_range_scatter_add_counts (ABI 10): the same out rows and flags as the sequential
+    restatement, reg_count[r] = the number of keys of row r for EVERY row (0 included, the buffer
+    starts as garbage), keys outside [0, nrows) flagged 0 and counted nowhere."""
+    from lgcn_amd import _ffi
+
+    lib = _ffi.load()
+    rng = np.random.default_rng(B + nrows + 1)
+    keys_np = rng.integers(0, nrows, B)
+    if bad:
+        keys_np[::97] = nrows + 3
+        keys_np[1::89] = -2
+    off = 11
+    N = off + nrows + 3
+    mul, div = float(np.float32(1 / 4)), 4.0
+    C = rng.standard_normal((B, d)).astype(np.float32)
+    out0 = rng.standard_normal((N, d)).astype(np.float32)
+    split = off + nrows // 2
+    lo = torch.from_numpy(out0[:split].copy()).to(gpu)
+    hi = torch.from_numpy(out0[split:].copy()).to(gpu)
+    keys = torch.from_numpy(keys_np.astype(np.int64)).to(gpu)
+    Cg = torch.from_numpy(C).to(gpu)
+    flag = torch.full((B,), 7, dtype=torch.uint8, device=gpu)
+    cnt = torch.full((nrows,), -5, dtype=torch.int32, device=gpu)
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    s = _ffi.stream_of(gpu)
+    _ffi.check(lib.lgcn_range_scatter_add_counts(keys.data_ptr(), B, nrows, off, Cg.data_ptr(), d, lo.data_ptr(),
+                                                 hi.data_ptr(), split, mul, div, flag.data_ptr(), ovf.data_ptr(), None,
+                                                 cnt.data_ptr(), None, 0, 0, 0.0, None, None, 0.0, s),
+               "lgcn_range_scatter_add_counts")
+    assert int(ovf.item()) == 0
+    inside = (keys_np >= 0) & (keys_np < nrows)
+    ref, rows = _ref_scatter(keys_np[inside], C[inside], out0, off, mul, div)
+    np.testing.assert_array_equal(torch.cat([lo, hi]).cpu().numpy(), ref)
+    np.testing.assert_array_equal(cnt.cpu().numpy(), np.bincount(keys_np[inside], minlength=nrows))
+    idx = np.nonzero(inside)[0]
+    firsts = sorted(int(idx[bs[0]]) for bs in rows.values())
+    np.testing.assert_array_equal(np.nonzero(flag.cpu().numpy())[0], firsts)
+    assert set(np.unique(flag.cpu().numpy())) <= {0, 1}
+
+
 def test_range_scatter_empty_and_single_row(gpu):
     # B = 0 is a no-op
     C, C2, out0, after1, after2, ovf, _ = _run(gpu, np.zeros(0, np.int64), 10, 0, 64, 10, 1.0, 1.0)
