@@ -38,7 +38,7 @@ extern "C" {
 
 typedef void* lgcn_stream_t; /* a hipStream_t; NULL = the null stream */
 
-#define LGCN_ABI_VERSION 10
+#define LGCN_ABI_VERSION 11
 
 #define LGCN_OK 0
 #define LGCN_E_ARG (-1)         /* bad size / null pointer / unsupported argument */
@@ -713,6 +713,22 @@ int lgcn_rows_gather(const float* p_lo, const float* p_hi, int64_t split, int32_
                      float* rows, int32_t scatter, lgcn_stream_t stream);
 int lgcn_rows_mark(const int64_t* ids, const uint8_t* first, int64_t n, uint8_t* mask, int32_t value,
                    lgcn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Launch programs (ABI 11): a captured hipGraph issued as plain launches on a stream.
+ * The fused Cluster-GCN step (reference utils/train_test.py:86-101, one batch) is captured once
+ * per batch; hipGraphLaunch costs the GPU ~8 us of its own per replay, the same kernels launched
+ * on the stream run back to back. lgcn_program_from_graph reads a graph's nodes once (kernels:
+ * function, grid, block, dynamic LDS and the node's own argument buffers; memsets; empty nodes
+ * dropped) in a dependency order (ready nodes lowest index first, so a one-stream
+ * capture keeps its order); lgcn_program_run issues them on `stream` in that order, from one call,
+ * no sync. The graph (hipGraph_t) must outlive the program: its nodes own the argument buffers.
+ * A graph holding copy, event, host or child-graph nodes, or a kernel launched with `extra`
+ * arguments, is refused with LGCN_E_UNSUPPORTED (the caller keeps replaying the graph). Host calls. */
+int lgcn_program_from_graph(void* graph, void** prog_out);
+int lgcn_program_launches(const void* prog);  /* kernels + memsets it issues per run */
+int lgcn_program_run(const void* prog, lgcn_stream_t stream);
+int lgcn_program_free(void* prog);
 
 /* ---------------------------------------------------------------------------------------
  * Host-side (no GPU): balanced k-way node partition for Cluster-GCN batching, the METIS

@@ -25,7 +25,7 @@ E_ARG, E_WORKSPACE, E_UNSUPPORTED = -1, -2, -3  # include/lgcn.h LGCN_E_*
 
 ITEM_BYTES = 16   # lgcn_item_t {int64 beg; int32 len; int32 dst}
 SPLIT_BYTES = 16  # lgcn_split_t {int32 row, pbeg, pcnt, pad}
-ABI_VERSION = 10  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
+ABI_VERSION = 11  # LGCN_ABI_VERSION of include/lgcn.h this binding speaks
 DIGEST_BLOCKS = 1024  # LGCN_DIGEST_BLOCKS
 
 _lib = None
@@ -140,6 +140,10 @@ _SIGS = {
     "lgcn_grad_norm": ([_vp, _i32, _f32, _vp, _vp, _vp], ctypes.c_int),
     "lgcn_adam_step": ([_vp, _i32, _f32, _f32, _f32, _f32, _f32, _f32, _vp, _vp, _i32, _vp], ctypes.c_int),
     "lgcn_adam_prologue": ([_vp, _f32, ctypes.c_double, ctypes.c_double, _vp, _vp], ctypes.c_int),
+    "lgcn_program_from_graph": ([_vp, ctypes.POINTER(_vp)], ctypes.c_int),
+    "lgcn_program_launches": ([_vp], ctypes.c_int),
+    "lgcn_program_run": ([_vp, _vp], ctypes.c_int),
+    "lgcn_program_free": ([_vp], ctypes.c_int),
     "lgcn_partition_edges": ([_vp, _vp, _i64, _i64, _i32, _i32, _f32, _vp], ctypes.c_int),
     "lgcn_partition_last_error": ([], ctypes.c_char_p),
 }
@@ -216,7 +220,7 @@ CSRC = _HERE.parent / "csrc"
 INCLUDE = _HERE.parent.parent / "include"
 # the translation units of liblgcn.so (lgcn_build.cpp carries the hash and is not hashed)
 SOURCES = ("lgcn_plan.hip", "lgcn_spmm.hip", "lgcn_optim.hip", "lgcn_bpr.hip", "lgcn_recall.hip", "lgcn_rowadam.hip",
-           "lgcn_exchange.hip", "lgcn_partition.cpp", "lgcn_sample.cpp", "lgcn_tuning.cpp")
+           "lgcn_exchange.hip", "lgcn_partition.cpp", "lgcn_sample.cpp", "lgcn_tuning.cpp", "lgcn_program.cpp")
 # the headers they include (csrc/), hashed and tracked as build dependencies with include/lgcn.h
 HEADERS = ("lgcn_common.h", "lgcn_exact.h", "lgcn_reg.h")
 

@@ -141,6 +141,47 @@ class _SegmentedGraph:
                 self.colls[i]()
 
 
+class StepProgram:
+    """A captured step issued as plain launches on the current stream (lgcn_program_run, ABI 11)
+    instead of a hipGraph replay: the graph's kernels, memsets and copies, read once from the
+    captured graph, launched from one C call. Measured (tools/train_eager_pair.sh,
+    profiles/r06zf_eager/): a hipGraph replay costs the GPU ~8 us of its own per step (the eager
+    step's kernels run back to back: C3 0.143 vs 0.151 ms, planted 0.445 vs 0.451 ms), but the
+    eager step's Python issue takes 0.130 ms — nearly the step. The program issues the captured
+    launches with neither cost. `graph` is a torch.cuda.CUDAGraph(keep_graph=True) after capture:
+    it is kept (its nodes own the argument buffers, its pool the step's buffers) and only replayed
+    as a graph if the library refuses it (a node with no stream-launch form)."""
+
+    def __init__(self, graph):
+        import ctypes
+
+        self.graph = graph
+        self._h = None
+        lib = _ffi.load()
+        h = ctypes.c_void_p()
+        rc = lib.lgcn_program_from_graph(graph.raw_cuda_graph(), ctypes.byref(h))
+        if rc == _ffi.E_UNSUPPORTED:
+            self.refused = lib.lgcn_last_error().decode(errors="replace")
+            self.launches = None
+            return
+        _ffi.check(rc, "lgcn_program_from_graph")
+        self.refused = None
+        self._h = h.value
+        self.launches = int(lib.lgcn_program_launches(self._h))
+
+    def replay(self) -> None:
+        if self._h is None:
+            self.graph.replay()
+            return
+        _ffi.check(_ffi.load().lgcn_program_run(self._h, torch.cuda.current_stream().cuda_stream),
+                   "lgcn_program_run")
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h is not None and _ffi._lib is not None:
+            _ffi._lib.lgcn_program_free(h)
+
+
 def batch_chunk_for(edges: int) -> int:
     """Hub chunk of a batch's propagation plan (edges: the batch's directed edges) and of its fixed
     gradient rows' segment plans (edges: their 2B contributions). Short chunks while the batch is small (its item
@@ -852,7 +893,11 @@ class FusedTrainStep:
                 loss = self._step_lazy(st)  # real first step (warms allocations), then capture
                 torch.cuda.synchronize()
                 steps = self.optimizer.steps
-                g = torch.cuda.CUDAGraph()
+                from . import tuning
+
+                # one-GPU step: issued as a launch program (StepProgram) unless tuned off
+                program = tuning.get().step_program and self.exchange is None and self.cols is None
+                g = torch.cuda.CUDAGraph(keep_graph=True) if program else torch.cuda.CUDAGraph()
                 # the capture records the launches of the step just run and runs none: its
                 # max_steps check is taken at that step's index (one past it fails when the
                 # constant table is exactly full), and the count is restored after
@@ -877,7 +922,7 @@ class FusedTrainStep:
                             self._lazy_update(st)
                 finally:
                     self.optimizer.steps = steps
-                st.graph = g
+                st.graph = StepProgram(g) if program else g
                 return loss
             if self.optimizer.steps + 1 > self.optimizer.max_steps:
                 raise RuntimeError("RowLazyAdam: max_steps exceeded")

@@ -54,6 +54,10 @@ class Tuning:
     # single-GPU lazy step: the BPR reg-gradient rows formed inside the clip norm and the Adam update
     # from their occurrence counts (lgcn_row_*_reg, bitwise) instead of two passes after the backward
     reg_in_update: bool = True
+    # a captured single-GPU training step is issued as a launch program (lgcn_program_run: the
+    # graph's kernels launched on the stream from one call, no hipGraphLaunch) instead of replayed
+    # as a hipGraph (~8 us of GPU time per replay)
+    step_program: bool = False
     # run the exchanges' RCCL branches even on a gloo group (tests: gloo carries the bytes)
     device_collectives: bool = False
     # --- native (lgcn_tuning_t) -----------------------------------------------------------------

@@ -44,7 +44,7 @@ def test_abi_version_and_error_codes():
     from lgcn_amd import _ffi
 
     lib = _ffi.load()
-    assert lib.lgcn_abi_version() == _ffi.ABI_VERSION == 10
+    assert lib.lgcn_abi_version() == _ffi.ABI_VERSION == 11
     b = ctypes.c_size_t(0)
     assert lib.lgcn_csr_workspace_size(-1, 5, ctypes.byref(b)) == -1
     assert b"bad args" in lib.lgcn_last_error()
@@ -58,6 +58,19 @@ def test_abi_version_and_error_codes():
     assert rc == -1 and b"bad mode" in lib.lgcn_last_error()
     with pytest.raises(_ffi.LgcnError):
         _ffi.check(-1, "probe")
+
+
+def test_launch_program_entry_points_refuse_nulls():
+    """ABI 11's launch programs check their arguments before any HIP call."""
+    from lgcn_amd import _ffi
+
+    lib = _ffi.load()
+    h = ctypes.c_void_p()
+    assert lib.lgcn_program_from_graph(None, ctypes.byref(h)) == _ffi.E_ARG and h.value is None
+    assert b"null" in lib.lgcn_last_error()
+    assert lib.lgcn_program_run(None, None) == _ffi.E_ARG
+    assert lib.lgcn_program_launches(None) == _ffi.E_ARG
+    assert lib.lgcn_program_free(None) == 0
 
 
 def test_product_path_fails_loudly_without_gpu():
