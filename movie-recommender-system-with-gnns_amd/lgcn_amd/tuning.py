@@ -57,7 +57,7 @@ class Tuning:
     # a captured single-GPU training step is issued as a launch program (lgcn_program_run: the
     # graph's kernels launched on the stream from one call, no hipGraphLaunch) instead of replayed
     # as a hipGraph (~8 us of GPU time per replay)
-    step_program: bool = False
+    step_program: bool = True
     # run the exchanges' RCCL branches even on a gloo group (tests: gloo carries the bytes)
     device_collectives: bool = False
     # --- native (lgcn_tuning_t) -----------------------------------------------------------------

@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_program.py tests/test_gpu_t
 for g in ml25m planted; do
   for i in 1 2; do
     timeout -k 10 300 python -u bench.py --workload train --graph $g --steps 200 --warmup 20 --no-cpu-baseline \
-      $([ $g = planted ] && echo --no-harness) > "$O/${g}_program_$i.log" 2>&1 || exit $?
+      --tune step_program=1 $([ $g = planted ] && echo --no-harness) > "$O/${g}_program_$i.log" 2>&1 || exit $?
     timeout -k 10 300 python -u bench.py --workload train --graph $g --steps 200 --warmup 20 --no-cpu-baseline \
       --no-harness --tune step_program=0 > "$O/${g}_graph_$i.log" 2>&1 || exit $?
   done
