@@ -110,9 +110,10 @@ class _SegmentedGraph:
     def __init__(self):
         self.graphs, self.colls = [], []
         self.pool = torch.cuda.graph_pool_handle()
+        self.program = _programs_on()  # each segment issued as a launch program (StepProgram)
 
     def _begin(self) -> None:
-        g = torch.cuda.CUDAGraph()
+        g = _new_graph(self.program)
         g.capture_begin(pool=self.pool)
         self.graphs.append(g)
 
@@ -132,6 +133,7 @@ class _SegmentedGraph:
             finally:
                 self.graphs[-1].capture_end()
         torch.cuda.current_stream().wait_stream(side)
+        self.graphs = [_replayable(g, self.program) for g in self.graphs]
         return out
 
     def replay(self) -> None:
@@ -180,6 +182,22 @@ class StepProgram:
         h, self._h = getattr(self, "_h", None), None
         if h is not None and _ffi._lib is not None:
             _ffi._lib.lgcn_program_free(h)
+
+
+def _programs_on() -> bool:
+    from . import tuning
+
+    return tuning.get().step_program
+
+
+def _new_graph(program: bool):
+    """A CUDAGraph to capture into: kept after capture (not instantiated) when it will be issued as
+    a launch program (StepProgram needs the graph's nodes)."""
+    return torch.cuda.CUDAGraph(keep_graph=True) if program else torch.cuda.CUDAGraph()
+
+
+def _replayable(g, program: bool):
+    return StepProgram(g) if program else g
 
 
 def batch_chunk_for(edges: int) -> int:
@@ -769,10 +787,11 @@ class FusedTrainStep:
             loss = self._lazy_grads(st, draw=False)
             if use_graphs:
                 torch.cuda.synchronize()
-                g = torch.cuda.CUDAGraph()
+                program = _programs_on()
+                g = _new_graph(program)
                 with torch.cuda.graph(g):
                     st.graph_loss = self._lazy_grads(st, draw=False)
-                st.graph = g
+                st.graph = _replayable(g, program)
         # the next step's rows: its batch's touched rows and its negatives, drawn now
         ex.mine.fill_(-1)
         if nxt is not None:
@@ -810,7 +829,8 @@ class FusedTrainStep:
             # the owner's two halves touch only the exchange buffers: one capture serves every batch
             torch.cuda.synchronize()
             steps = opt.steps
-            g0, g1 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            program = _programs_on()
+            g0, g1 = _new_graph(program), _new_graph(program)
             # the capture records the launches of the step just run and runs none: its max_steps
             # check is taken at that step's index (not one past it, which fails when the table is
             # exactly full), and the count is restored after
@@ -822,7 +842,7 @@ class FusedTrainStep:
                     self._owner_update()
             finally:
                 opt.steps = steps
-            self._owner_graphs = (g0, g1)
+            self._owner_graphs = (_replayable(g0, program), _replayable(g1, program))
         ex.pending = nxt
         self._synced = False
         self._k += 1
@@ -893,11 +913,9 @@ class FusedTrainStep:
                 loss = self._step_lazy(st)  # real first step (warms allocations), then capture
                 torch.cuda.synchronize()
                 steps = self.optimizer.steps
-                from . import tuning
-
-                # one-GPU step: issued as a launch program (StepProgram) unless tuned off
-                program = tuning.get().step_program and self.exchange is None and self.cols is None
-                g = torch.cuda.CUDAGraph(keep_graph=True) if program else torch.cuda.CUDAGraph()
+                # issued as launch programs (StepProgram) unless tuned off
+                program = _programs_on()
+                g = _new_graph(program)
                 # the capture records the launches of the step just run and runs none: its
                 # max_steps check is taken at that step's index (one past it fails when the
                 # constant table is exactly full), and the count is restored after
@@ -917,12 +935,13 @@ class FusedTrainStep:
                     else:  # two halves: the all_gather between them runs eagerly
                         with torch.cuda.graph(g):
                             st.graph_loss = self._lazy_grads(st, draw=False)
-                        st.graph_post = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(st.graph_post):
+                        post = _new_graph(program)
+                        with torch.cuda.graph(post):
                             self._lazy_update(st)
+                        st.graph_post = _replayable(post, program)
                 finally:
                     self.optimizer.steps = steps
-                st.graph = StepProgram(g) if program else g
+                st.graph = g if isinstance(g, _SegmentedGraph) else _replayable(g, program)
                 return loss
             if self.optimizer.steps + 1 > self.optimizer.max_steps:
                 raise RuntimeError("RowLazyAdam: max_steps exceeded")

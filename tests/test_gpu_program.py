@@ -134,3 +134,44 @@ def test_step_program_bitwise_graph_replay_and_eager(gpu, min_b, clip):
         assert runs[mode][0] == runs["eager"][0], mode
         for x, y in zip(runs[mode][1], runs["eager"][1]):
             assert torch.equal(x, y), mode
+
+
+def _train_exchange(gpu, program: bool, steps=12):
+    import graphs
+    from lgcn_amd import cluster as C
+    from lgcn_amd import distributed as D
+    from lgcn_amd import tuning
+    from lgcn_amd.optim import RowLazyAdam
+    from lgcn_amd.train_step import FusedTrainStep, StepProgram
+    from models.light_gcn import LightGCN
+
+    U, I, ei = graphs.subsampled(U=2000, I=1000, pairs=8000, seed=4)
+    part = C.partition_nodes(ei, U + I, 8)
+    batches = [_Batch(torch.from_numpy(x).to(gpu)) for x in C.intra_part_edges(ei, part, 8)]
+    cap = D.exchange_capacity(batches, U)
+    with tuning.tuned(step_program=program):
+        torch.manual_seed(0)
+        m = LightGCN(U, I, num_layers=3, dim_h=64).to(gpu)
+        opt = RowLazyAdam(m.user_embedding.weight.data, m.item_embedding.weight.data, lr=1e-2, max_grad_norm=1.0)
+        step = FusedTrainStep(m, opt, graphs=True, lazy=True, exchange=D.RowExchange(cap, U + I, 64, gpu, 1))
+        losses = []
+        for i in range(steps):
+            torch.cuda.manual_seed(100 + i)
+            losses.append(step.step(batches[i % 8]).item())
+        step.sync()
+        if program:
+            for st in step._states.values():
+                for half in (st.graph, st.graph_post):
+                    assert isinstance(half, StepProgram)
+                    print("exchange step half:", half.launches, "launches" if half.refused is None else
+                          f"replayed as a graph ({half.refused})")
+        return losses, m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone()
+
+
+def test_exchange_step_halves_as_programs_bitwise_graph_replay(gpu):
+    """The data-parallel step's two captured halves (before / after the row exchange's all_gather,
+    one rank) issued as launch programs: bitwise their hipGraph replays."""
+    a = _train_exchange(gpu, program=False)
+    b = _train_exchange(gpu, program=True)
+    assert a[0] == b[0]
+    assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
