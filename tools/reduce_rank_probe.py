@@ -4,7 +4,8 @@ all_reduce (a stand-in reducer that moves nothing): the time a rank spends in it
 step, next to the bytes a ring all_reduce of its item partials moves per rank.
 python tools/reduce_rank_probe.py [--grids 2x1,4x1,8x1,2x2,4x2,2x4] [--orders overlapped,fused,fused-seq]
 A +g suffix (fused+g, ...) captures the step in a hipGraph once and times its replays (no host
-launch overhead).
+launch overhead). Eager orders also print the host's issue time per step (the Python loop before
+the synchronize; the stand-in reducer issues no collectives).
 An order suffixed -u (overlapped-u, fused-u) combines every split row with a workgroup of its own
 (n_split_big = -1) instead of packing the <= 16-chunk ones one per lane group."""
 import argparse
@@ -67,6 +68,7 @@ def main():
         c0, c1 = grid.cols
         shards = UserShards.build(deg, U, R)
         times, moved = {o: [] for o in args.orders.split(",")}, 0
+        host = {o: [] for o in times}  # the host's issue time per step (eager orders)
         for gr in sorted({0, R - 1}):
             rplan = ReducePlan(ei, shards, gr, c1 - c0, args.chunk)
             x0u, x0i = uw[:, c0:c1].contiguous(), iw[:, c0:c1].contiguous()
@@ -110,6 +112,7 @@ def main():
                         t = time.perf_counter()
                         for _ in range(args.steps):
                             propagate_forward_reduced(x0u, x0i, rplan, K, red, fused=fused)
+                        host[order].append((time.perf_counter() - t) / args.steps * 1e3)
                         torch.cuda.synchronize()
                         moved_per_step = red.bytes / args.steps
                 times[order].append((time.perf_counter() - t) / args.steps * 1e3)
@@ -120,7 +123,8 @@ def main():
         for order, ts in times.items():
             print(f"grid {R}x{F} reduce ({order}): rank compute {max(ts):.3f} ms/step (row groups "
                   f"{sorted({0, R - 1})}: {', '.join(f'{t:.3f}' for t in ts)}); ring all_reduce bytes per rank per "
-                  f"step {moved / 1e6:.1f} MB", flush=True)
+                  f"step {moved / 1e6:.1f} MB" + (f"; host issue {max(host[order]):.3f} ms/step (no collectives)"
+                                                   if host[order] else ""), flush=True)
 
 
 if __name__ == "__main__":
