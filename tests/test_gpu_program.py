@@ -175,3 +175,46 @@ def test_exchange_step_halves_as_programs_bitwise_graph_replay(gpu):
     b = _train_exchange(gpu, program=True)
     assert a[0] == b[0]
     assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+
+
+def test_program_orders_a_forked_capture(gpu):
+    """A capture that forks onto a second stream and joins again has two parallel branches; the
+    program issues them one after the other in a dependency order: the joined result equals the
+    eager sequence's, three runs in a row."""
+    from lgcn_amd.train_step import StepProgram
+
+    n = 1 << 16
+
+    def bufs():
+        torch.manual_seed(5)
+        return [torch.randn(n, device=gpu) for _ in range(3)]
+
+    side = torch.cuda.Stream(gpu)
+
+    def seq(a, b, c):
+        main = torch.cuda.current_stream(gpu)
+        side.wait_stream(main)
+        a.mul_(0.5).add_(1.0)          # branch 1 (main stream)
+        with torch.cuda.stream(side):
+            b.mul_(2.0).sub_(c)        # branch 2 (side stream)
+            c.add_(0.25)
+        main.wait_stream(side)
+        a.add_(b).mul_(c)              # the join reads both branches
+
+    ref = bufs()
+    for _ in range(3):
+        seq(*ref)
+    torch.cuda.synchronize()
+    got = bufs()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g):
+        seq(*got)
+    prog = StepProgram(g)
+    assert prog.refused is None, prog.refused
+    assert prog.launches == 7
+    for _ in range(3):
+        prog.replay()
+    torch.cuda.synchronize()
+    for x, y in zip(ref, got):
+        assert torch.equal(x, y)
