@@ -72,7 +72,8 @@ int lgcn_program_from_graph(void* graph, void** prog_out) {
     size_t n = 0;
     if (int rc = check_hip(hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes")) return rc;
     std::vector<hipGraphNode_t> nodes(n);
-    if (n && check_hip(hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes")) return static_cast<int>(hipErrorUnknown);
+    if (n)
+        if (int rc = check_hip(hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes")) return rc;
     nodes.resize(n);
     // dependency order (Kahn; among ready nodes the lowest index first, so a one-stream capture
     // keeps its issue order): every node is issued after all of its dependencies, on one stream
@@ -83,8 +84,10 @@ int lgcn_program_from_graph(void* graph, void** prog_out) {
         if (int rc = check_hip(hipGraphNodeGetDependencies(nodes[i], nullptr, &nd), "hipGraphNodeGetDependencies"))
             return rc;
         std::vector<hipGraphNode_t> deps(nd);
-        if (nd && check_hip(hipGraphNodeGetDependencies(nodes[i], deps.data(), &nd), "hipGraphNodeGetDependencies"))
-            return static_cast<int>(hipErrorUnknown);
+        if (nd)
+            if (int rc = check_hip(hipGraphNodeGetDependencies(nodes[i], deps.data(), &nd),
+                                   "hipGraphNodeGetDependencies"))
+                return rc;
         for (size_t j = 0; j < nd; ++j) {
             auto it = std::find(nodes.begin(), nodes.end(), deps[j]);
             if (it == nodes.end()) return fail(LGCN_E_ARG, "lgcn_program_from_graph: dependency outside the graph");
