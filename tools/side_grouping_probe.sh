@@ -1,6 +1,8 @@
 #!/bin/bash
 # Planted step: the negatives' grouping on a side stream (tuning grouping_side_stream) vs in line,
 # eagerly, as hipGraph replays and as launch programs.   bash tools/side_grouping_probe.sh TAG
+# (grouping_side_stream was a tuning field of the measured build only, reverted after this probe:
+# DESIGN §10 item 6, profiles/r06zq_side/)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 2
 O=gpurun_out/$1
