@@ -180,8 +180,11 @@ class StepProgram:
 
     def __del__(self):
         h, self._h = getattr(self, "_h", None), None
-        if h is not None and _ffi._lib is not None:
-            _ffi._lib.lgcn_program_free(h)
+        try:
+            if h is not None and _ffi._lib is not None:
+                _ffi._lib.lgcn_program_free(h)
+        except Exception:  # interpreter shutdown: the module may already be torn down
+            pass
 
 
 def _programs_on() -> bool:
