@@ -89,7 +89,13 @@ struct BprArgs {
 // column groups) and finish with them.
 constexpr int kBprFused = 0, kBprPartials = 1, kBprFromSums = 2;
 
-template <int LPR, int NV, int PHASE>
+// SPEC: the propagated rows of u, p and n are loaded beside the touched flags and the W rows, and
+// the flag then picks F or (W / div) * mul (one dependent load level fewer per triplet; the same
+// values). It pays on small batches, whose negatives mostly hit propagated rows; on large ones
+// (most negatives untouched) the extra F reads cost more (profiles/r06q_bpr_speculative/).
+constexpr int64_t kBprSpecMaxB = 49152;
+
+template <int LPR, int NV, int PHASE, bool SPEC = false>
 __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
     constexpr int GPB = kBlock / LPR;
     const int g = threadIdx.x / LPR;
@@ -107,9 +113,9 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
     const bool tu = a.touched == nullptr || a.touched[ru];
     const bool tp = a.touched == nullptr || a.touched[rp];
     const bool tn = a.touched == nullptr || a.touched[rn];
-    const float4* fu = tu ? reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, ru, d)) + l : wu;
-    const float4* fp = tp ? reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, rp, d)) + l : wp;
-    const float4* fn = tn ? reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, rn, d)) + l : wn;
+    const float4* fu = (SPEC || tu) ? reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, ru, d)) + l : wu;
+    const float4* fp = (SPEC || tp) ? reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, rp, d)) + l : wp;
+    const float4* fn = (SPEC || tn) ? reinterpret_cast<const float4*>(srow(a.f_lo, a.f_hi, a.f_split, rn, d)) + l : wn;
     float4 U_[NV], P_[NV], N_[NV], WU[NV], WP[NV], WN[NV];
     float suu = 0.f, spp = 0.f, snn = 0.f, sup = 0.f, sun = 0.f, sreg = 0.f;
 #pragma unroll
@@ -117,12 +123,17 @@ __global__ __launch_bounds__(kBlock) void k_bpr_fused(BprArgs a) {
         U_[k] = fu[k * LPR];
         P_[k] = fp[k * LPR];
         N_[k] = fn[k * LPR];
-        if (!tu) U_[k] = make_float4((U_[k].x / a.div) * a.mul, (U_[k].y / a.div) * a.mul, (U_[k].z / a.div) * a.mul, (U_[k].w / a.div) * a.mul);
-        if (!tp) P_[k] = make_float4((P_[k].x / a.div) * a.mul, (P_[k].y / a.div) * a.mul, (P_[k].z / a.div) * a.mul, (P_[k].w / a.div) * a.mul);
-        if (!tn) N_[k] = make_float4((N_[k].x / a.div) * a.mul, (N_[k].y / a.div) * a.mul, (N_[k].z / a.div) * a.mul, (N_[k].w / a.div) * a.mul);
         WU[k] = wu[k * LPR];
         WP[k] = wp[k * LPR];
         WN[k] = wn[k * LPR];
+        if constexpr (SPEC) {  // an untouched row's F is not the propagated value: take it from W
+            if (!tu) U_[k] = WU[k];
+            if (!tp) P_[k] = WP[k];
+            if (!tn) N_[k] = WN[k];
+        }
+        if (!tu) U_[k] = make_float4((U_[k].x / a.div) * a.mul, (U_[k].y / a.div) * a.mul, (U_[k].z / a.div) * a.mul, (U_[k].w / a.div) * a.mul);
+        if (!tp) P_[k] = make_float4((P_[k].x / a.div) * a.mul, (P_[k].y / a.div) * a.mul, (P_[k].z / a.div) * a.mul, (P_[k].w / a.div) * a.mul);
+        if (!tn) N_[k] = make_float4((N_[k].x / a.div) * a.mul, (N_[k].y / a.div) * a.mul, (N_[k].z / a.div) * a.mul, (N_[k].w / a.div) * a.mul);
         suu += dot4(U_[k], U_[k]);
         spp += dot4(P_[k], P_[k]);
         snn += dot4(N_[k], N_[k]);
@@ -764,9 +775,17 @@ int launch_bpr(const BprArgs& a, int phase, hipStream_t s) {
     const int64_t blocks = (a.B + GPB - 1) / GPB;
     if (blocks > 0) {
         const dim3 grid(static_cast<unsigned>(blocks));
-        if (phase == kBprPartials) k_bpr_fused<LPR, NV, kBprPartials><<<grid, kBlock, 0, s>>>(a);
-        else if (phase == kBprFromSums) k_bpr_fused<LPR, NV, kBprFromSums><<<grid, kBlock, 0, s>>>(a);
-        else k_bpr_fused<LPR, NV, kBprFused><<<grid, kBlock, 0, s>>>(a);
+        const bool spec = a.touched != nullptr && a.B < kBprSpecMaxB;
+        if (phase == kBprPartials) {
+            if (spec) k_bpr_fused<LPR, NV, kBprPartials, true><<<grid, kBlock, 0, s>>>(a);
+            else k_bpr_fused<LPR, NV, kBprPartials><<<grid, kBlock, 0, s>>>(a);
+        } else if (phase == kBprFromSums) {
+            if (spec) k_bpr_fused<LPR, NV, kBprFromSums, true><<<grid, kBlock, 0, s>>>(a);
+            else k_bpr_fused<LPR, NV, kBprFromSums><<<grid, kBlock, 0, s>>>(a);
+        } else {
+            if (spec) k_bpr_fused<LPR, NV, kBprFused, true><<<grid, kBlock, 0, s>>>(a);
+            else k_bpr_fused<LPR, NV, kBprFused><<<grid, kBlock, 0, s>>>(a);
+        }
     }
     return check_launch("k_bpr_fused");
 }
